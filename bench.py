@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark: decoded codewords/s for the n=18432 / m=2048 BP decoder at 50
+iterations (BASELINE.json metric), one process per GPU.
+
+    python bench.py                       # N=1, 100k synthetic codewords per step
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Workload (SURVEY 8(d) config 3, weak-scaled per GPU for configs 4): every
+rank decodes its own contiguous shard of `--batch-per-gpu` codewords
+[rank*B, (rank+1)*B) from the counter-based BSC(p=0.02) generator (transmitted
+word codeword_n18432_m1860_{1 + b mod 272}, LLR = +-ln49, LR = exp(LLR) by the
+host libm as DNA_main.cpp:1344 does).  p = 0.02 never converges, so every
+codeword runs exactly 50 iterations.  Inputs are generated into HBM before the
+timed region; a step = one full decode of the shard (init, 50 x [syndrome,
+check, variable], final syndrome, hard-bit unpack, iteration counts).
+
+No data-path collective: ranks only meet in a barrier and a MAX of their
+elapsed times (gloo, CPU tensors).  `value` = all codewords of all ranks /
+max elapsed.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "dna-ldpc-codes_amd")]
+
+METRIC = "decoded codewords/sec (n=18432, m=2048, 50 BP iters) at 1/2/4/8 GPUs; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch-per-gpu", type=int, default=100_000)
+    ap.add_argument("--max-iter", type=int, default=50)
+    ap.add_argument("--algo", default="bp", choices=["bp", "msa"])
+    ap.add_argument("--p", type=float, default=0.02)
+    ap.add_argument("--seed", type=int, default=2026)
+    ap.add_argument("--chunk", type=int, default=0, help="resident codewords per pass (0: auto)")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only (barrier + max); no GPU collectives
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist
+    return world, rank, local, pg
+
+
+def reduce_max(pg, x: float) -> float:
+    if pg is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def reduce_sum(pg, x: float) -> float:
+    if pg is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.SUM)
+    return float(t.item())
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def cpu_baseline(args, llr_fn, N):
+    """The oracle (bit-exact C restatement of dec.cpp, 'port') on the host cores,
+    on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    og = oracle.OracleGraph(os.path.join(ROOT, "tests", "golden", "decode_n18432_m2048_final.pchk"))
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        threads = os.cpu_count() or 1
+    threads = max(1, min(threads, 16))
+    algo = 0 if args.algo == "bp" else 1
+    # calibrate with one codeword per thread, then size the sample for ~cpu_seconds
+    llr = llr_fn(0, threads)
+    t = time.perf_counter()
+    og.decode_batch(llr, args.max_iter, algo=algo, threads=threads, want_post=False)
+    t1 = time.perf_counter() - t
+    per_round = max(t1, 1e-3)
+    rounds = max(1, int(args.cpu_seconds / per_round))
+    n = threads * rounds
+    llr = llr_fn(threads, n)
+    t = time.perf_counter()
+    og.decode_batch(llr, args.max_iter, algo=algo, threads=threads, want_post=False)
+    el = time.perf_counter() - t
+    return {"value": round(n / el, 3), "unit": "codewords/s", "cores": threads, "kind": "port",
+            "sample": f"{n} codewords of the same BSC(p={args.p}) workload (indices {threads}..{threads + n - 1}), "
+                      f"{args.max_iter} iters, oracle/ldpc_oracle.c on {threads} host threads, {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    world, rank, local, pg = dist_setup(args)
+    import ldpc_amd as L
+    import synth
+
+    G = L.Graph(synth.PCHK)
+    N, E = G.N, G.E
+    B = args.batch_per_gpu
+    dev = local
+    algo = args.algo
+    eng = L.Engine(G, dev, algo, chunk=args.chunk)
+    cw = synth.load_codewords()
+    d_cw = L.DeviceBuffer(dev, cw.nbytes)
+    d_cw.upload(cw)
+    in_kind = L.IN_LR if algo == "bp" else L.IN_LLR
+    d_in = L.DeviceBuffer(dev, B * N * 8)
+    b0 = rank * B
+    eng.gen_bsc(d_in.at(0), in_kind, b0, B, d_cw.at(0), cw.shape[0], args.seed, args.p, synth.LLR_UNIT)
+    d_hard = L.DeviceBuffer(dev, B * N)
+    d_iters = L.DeviceBuffer(dev, B * 4)
+    d_valid = L.DeviceBuffer(dev, B)
+    eng.sync()
+
+    def step():
+        eng.decode(d_in.at(0), in_kind, B, args.max_iter, d_hard.at(0), None, L.POST_LLR, d_iters.at(0),
+                   d_valid.at(0))
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    eng.profile(not args.no_profile)
+    barrier(pg)
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.sync()
+    el = time.perf_counter() - t0
+    barrier(pg)
+    el_max = reduce_max(pg, el)
+    st = eng.stats()
+    iters = d_iters.download(np.empty(B, np.int32))
+    valid = d_valid.download(np.empty(B, np.uint8))
+    total_cw = reduce_sum(pg, float(B * args.steps))
+    value = total_cw / el_max
+
+    # ---- roofline of the dominant kernel (algorithmic bytes) ----
+    cw_iters = float(iters.sum()) * args.steps  # executed codeword-iterations (this rank)
+    by_kernel = {
+        # check phase: read E v->c (d) + write E c->v (lr), fp64
+        "check": 16.0 * E,
+        # variable phase: read E lr + N LR, write E d + N/8 hard-bit ballots
+        "variable": 16.0 * E + 8.0 * N + N / 8.0,
+    }
+    dom = max(("check", "variable"), key=lambda k: st[k]["ms"])
+    k_ms = st[dom]["ms"]
+    k_launch = max(1, st[dom]["launches"])
+    bytes_total = by_kernel[dom] * cw_iters
+    achieved = bytes_total / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
+    it_ms = st["check"]["ms"] + st["variable"]["ms"] + st["syndrome"]["ms"]
+    iter_bytes = (32.0 * E + 10.0 * N) * cw_iters
+    roof = {
+        "bound": "hbm", "kernel": f"k_{'check' if dom == 'check' else 'var'}_{algo}",
+        "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": None,
+        "bytes_per_launch": round(bytes_total / k_launch), "avg_launch_ms": round(k_ms / k_launch, 4),
+        "iteration_GBps": round(iter_bytes / (it_ms * 1e-3) / 1e9, 1) if it_ms > 0 else None,
+        "kernel_ms": {k: round(v["ms"], 2) for k, v in st.items()},
+        "launches": {k: v["launches"] for k, v in st.items()},
+    }
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "codewords/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el_max / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"bsc-p{args.p}-{B // 1000}k-per-gpu-{algo}{args.max_iter}",
+                   "code": "decode_n18432_m2048_final.pchk (8,72)-regular, E=147456",
+                   "batch_per_gpu": B, "global_batch": int(total_cw / args.steps), "max_iter": args.max_iter,
+                   "algo": algo, "parallelism": f"dp{world} (contiguous codeword shards, no collective)",
+                   "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 4)},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        def llr_fn(start, n):
+            return synth.bsc_llrs(cw, b0 + start, n, seed=args.seed, p=args.p)
+        out["cpu_baseline"] = cpu_baseline(args, llr_fn, N)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

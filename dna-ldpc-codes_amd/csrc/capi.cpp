@@ -1,0 +1,369 @@
+// capi.cpp -- the extern "C" boundary declared in include/ldpc_amd.h.
+//
+// Host side of the drop-in for ldpc.exe: graph handles (immutable, shared),
+// a per-graph pool of device engines + pinned staging buffers (so repeated
+// calls from decoder.py do not re-allocate), host-side exp() exactly as the
+// reference (DNA_main.cpp:1344), and one host thread per GPU for multi-device
+// calls -- contiguous codeword shards, no collective (the reference's dormant
+// per-rank frame split, DNA_main.cpp:629-651, with its MPI_Reduce of counters,
+// DNA_main.cpp:1187-1193, reduced to a host gather).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/ldpc_amd.h"
+#include "engine.hpp"
+#include "graph.hpp"
+
+using ldpc::Engine;
+using ldpc::HostGraph;
+using ldpc::set_error;
+
+namespace {
+
+// One reusable device context for host-buffer decodes.
+struct Slot {
+    std::unique_ptr<Engine> eng;
+    int device = 0, algo = 0;
+    int64_t cap = 0;
+    double* h_in = nullptr;   // pinned [cap][N]
+    double* h_post = nullptr; // pinned [cap][N]
+    uint8_t* h_hard = nullptr;
+    int32_t* h_iters = nullptr;
+    uint8_t* h_valid = nullptr;
+    double* d_in = nullptr;
+    double* d_post = nullptr;
+    uint8_t* d_hard = nullptr;
+    int32_t* d_iters = nullptr;
+    uint8_t* d_valid = nullptr;
+
+    ~Slot()
+    {
+        if (eng) hipSetDevice(device);
+        hipHostFree(h_in); hipHostFree(h_post); hipHostFree(h_hard); hipHostFree(h_iters); hipHostFree(h_valid);
+        hipFree(d_in); hipFree(d_post); hipFree(d_hard); hipFree(d_iters); hipFree(d_valid);
+        eng.reset();
+    }
+};
+
+int make_slot(const HostGraph* g, int device, int algo, int64_t cap, std::unique_ptr<Slot>& out)
+{
+    auto s = std::make_unique<Slot>();
+    s->device = device;
+    s->algo = algo;
+    s->eng = std::make_unique<Engine>();
+    int rc = s->eng->init(g, device, algo, cap);
+    if (rc) return rc;
+    s->cap = s->eng->cap;
+    const size_t N = (size_t)g->N, C = (size_t)s->cap;
+    LDPC_HIP(hipHostMalloc((void**)&s->h_in, C * N * sizeof(double), hipHostMallocDefault));
+    LDPC_HIP(hipHostMalloc((void**)&s->h_post, C * N * sizeof(double), hipHostMallocDefault));
+    LDPC_HIP(hipHostMalloc((void**)&s->h_hard, C * N, hipHostMallocDefault));
+    LDPC_HIP(hipHostMalloc((void**)&s->h_iters, C * sizeof(int32_t), hipHostMallocDefault));
+    LDPC_HIP(hipHostMalloc((void**)&s->h_valid, C, hipHostMallocDefault));
+    LDPC_HIP(hipMalloc((void**)&s->d_in, C * N * sizeof(double)));
+    LDPC_HIP(hipMalloc((void**)&s->d_post, C * N * sizeof(double)));
+    LDPC_HIP(hipMalloc((void**)&s->d_hard, C * N));
+    LDPC_HIP(hipMalloc((void**)&s->d_iters, C * sizeof(int32_t)));
+    LDPC_HIP(hipMalloc((void**)&s->d_valid, C));
+    out = std::move(s);
+    return LDPC_OK;
+}
+
+template <typename F>
+void parallel_rows(int64_t n, int threads, F&& f)
+{
+    threads = (int)std::max<int64_t>(1, std::min<int64_t>(threads, n));
+    if (threads == 1) { f(0, n); return; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) th.emplace_back([&, t] { f(n * t / threads, n * (t + 1) / threads); });
+    for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+struct ldpc_graph {
+    HostGraph h;
+    std::mutex mu;
+    std::vector<std::unique_ptr<Slot>> free_slots;
+
+    std::unique_ptr<Slot> take(int device, int algo, int64_t need)
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (size_t i = 0; i < free_slots.size(); i++) {
+            auto& s = free_slots[i];
+            if (s->device == device && s->algo == algo && s->cap >= need) {
+                auto r = std::move(s);
+                free_slots.erase(free_slots.begin() + (long)i);
+                return r;
+            }
+        }
+        return nullptr;
+    }
+    void give(std::unique_ptr<Slot> s)
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        // keep at most a few idle slots per graph
+        if (free_slots.size() >= 8) free_slots.erase(free_slots.begin());
+        free_slots.push_back(std::move(s));
+    }
+};
+
+struct ldpc_engine {
+    std::unique_ptr<Engine> e;
+};
+
+static int fail(int rc, int* err)
+{
+    if (err) *err = rc;
+    return rc;
+}
+
+extern "C" {
+
+int ldpc_abi_version(void) { return LDPC_AMD_ABI_VERSION; }
+
+const char* ldpc_last_error(void) { return ldpc::last_error(); }
+
+int ldpc_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+ldpc_graph* ldpc_graph_load(const char* pchk_path, int* err)
+{
+    if (!pchk_path) { set_error("null path"); fail(LDPC_ERR_ARG, err); return nullptr; }
+    auto g = std::make_unique<ldpc_graph>();
+    std::string msg;
+    int rc = ldpc::load_pchk(pchk_path, g->h, &msg);
+    if (rc) { set_error(msg); fail(rc, err); return nullptr; }
+    if (err) *err = LDPC_OK;
+    return g.release();
+}
+
+ldpc_graph* ldpc_graph_from_edges(int32_t M, int32_t N, const int32_t* rows, const int32_t* cols, int64_t n_edges,
+                                  int* err)
+{
+    if ((!rows || !cols) && n_edges > 0) { set_error("null edge arrays"); fail(LDPC_ERR_ARG, err); return nullptr; }
+    auto g = std::make_unique<ldpc_graph>();
+    std::string msg;
+    int rc = ldpc::build_graph(M, N, rows, cols, n_edges, g->h, &msg);
+    if (rc) { set_error(msg); fail(rc, err); return nullptr; }
+    if (err) *err = LDPC_OK;
+    return g.release();
+}
+
+void ldpc_graph_free(ldpc_graph* g) { delete g; }
+
+int ldpc_graph_info(const ldpc_graph* g, int32_t* M, int32_t* N, int64_t* E, int32_t* dv_max, int32_t* regular_dv,
+                    int32_t* dc_max, int32_t* regular_dc)
+{
+    if (!g) { set_error("null graph"); return LDPC_ERR_ARG; }
+    if (M) *M = g->h.M;
+    if (N) *N = g->h.N;
+    if (E) *E = g->h.E;
+    if (dv_max) *dv_max = g->h.dv_max;
+    if (regular_dv) *regular_dv = g->h.regular_dv;
+    if (dc_max) *dc_max = g->h.dc_max;
+    if (regular_dc) *regular_dc = g->h.regular_dc;
+    return LDPC_OK;
+}
+
+int ldpc_graph_edges(const ldpc_graph* g, int32_t* row_ptr, int32_t* col_idx, int32_t* col_ptr, int32_t* col_edge)
+{
+    if (!g) { set_error("null graph"); return LDPC_ERR_ARG; }
+    const auto& h = g->h;
+    if (row_ptr) std::memcpy(row_ptr, h.row_ptr.data(), h.row_ptr.size() * 4);
+    if (col_idx) std::memcpy(col_idx, h.col_idx.data(), h.col_idx.size() * 4);
+    if (col_ptr) std::memcpy(col_ptr, h.col_ptr.data(), h.col_ptr.size() * 4);
+    if (col_edge) std::memcpy(col_edge, h.col_edge.data(), h.col_edge.size() * 4);
+    return LDPC_OK;
+}
+
+int ldpc_graph_syndrome(const ldpc_graph* g, const uint8_t* dblk, uint8_t* pchk)
+{
+    if (!g || !dblk) { set_error("null argument"); return LDPC_ERR_ARG; }
+    return ldpc::syndrome_host(g->h, dblk, pchk);
+}
+
+int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_iter, int32_t algo,
+                uint8_t* hard_out, double* post_out, int32_t* iters_out, uint8_t* valid_out, const ldpc_opts* opts)
+{
+    ldpc_graph* g = const_cast<ldpc_graph*>(gc);
+    if (!g) { set_error("null graph"); return LDPC_ERR_ARG; }
+    if (B < 0 || max_iter < 0) { set_error("B and max_iter must be >= 0"); return LDPC_ERR_ARG; }
+    if (B > 0 && (!llr || !hard_out)) { set_error("llr and hard_out are required"); return LDPC_ERR_ARG; }
+    if (algo != LDPC_ALGO_BP && algo != LDPC_ALGO_MSA) { set_error("unknown algorithm"); return LDPC_ERR_ARG; }
+    ldpc_opts o{};
+    o.exp_on_host = 1;
+    if (opts) o = *opts;
+    if (algo == LDPC_ALGO_MSA && post_out && o.post_kind == LDPC_POST_RATIO) {
+        set_error("LDPC_POST_RATIO is BP-only");
+        return LDPC_ERR_ARG;
+    }
+    if (B == 0) return LDPC_OK;
+
+    std::vector<int> devs;
+    const int ndev = std::max(1, (int)o.n_devices);
+    for (int i = 0; i < ndev; i++) devs.push_back(o.devices ? o.devices[i] : i);
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int host_threads = o.host_threads > 0 ? o.host_threads : std::min(8, std::max(1, hw / ndev));
+    const size_t N = (size_t)g->h.N;
+
+    std::vector<int> rcs(devs.size(), LDPC_OK);
+    std::vector<std::string> msgs(devs.size());
+    auto work = [&](size_t di) {
+        const int dev = devs[di];
+        const int64_t s0 = B * (int64_t)di / (int64_t)devs.size();
+        const int64_t s1 = B * (int64_t)(di + 1) / (int64_t)devs.size();
+        const int64_t shard = s1 - s0;
+        if (shard <= 0) return;
+        int64_t chunk = o.chunk > 0 ? o.chunk : 4096;
+        chunk = std::min<int64_t>(chunk, (shard + 63) / 64 * 64);
+        std::unique_ptr<Slot> slot = g->take(dev, algo, chunk);
+        int rc = LDPC_OK;
+        if (!slot) rc = make_slot(&g->h, dev, algo, chunk, slot);
+        if (rc) { rcs[di] = rc; msgs[di] = ldpc::last_error(); return; }
+        Engine& E = *slot->eng;
+        const bool host_exp = (algo == LDPC_ALGO_BP) && o.exp_on_host;
+        const int in_kind = (algo == LDPC_ALGO_BP && host_exp) ? LDPC_IN_LR : LDPC_IN_LLR;
+        for (int64_t b0 = s0; b0 < s1 && rc == LDPC_OK; b0 += slot->cap) {
+            const int64_t Bc = std::min<int64_t>(slot->cap, s1 - b0);
+            const double* src = llr + (size_t)b0 * N;
+            if (host_exp)  // DNA_main.cpp:1344  g_received_LR[i] = exp(g_received_LLR[i])
+                parallel_rows(Bc, host_threads, [&](int64_t r0, int64_t r1) {
+                    for (size_t i = (size_t)r0 * N; i < (size_t)r1 * N; i++) slot->h_in[i] = std::exp(src[i]);
+                });
+            else
+                parallel_rows(Bc, host_threads, [&](int64_t r0, int64_t r1) {
+                    std::memcpy(slot->h_in + (size_t)r0 * N, src + (size_t)r0 * N, (size_t)(r1 - r0) * N * 8);
+                });
+            auto step = [&]() -> int {
+                LDPC_HIP(hipSetDevice(dev));
+                LDPC_HIP(hipMemcpyAsync(slot->d_in, slot->h_in, (size_t)Bc * N * 8, hipMemcpyHostToDevice, E.stream));
+                int r = E.run_chunk(slot->d_in, in_kind, Bc, max_iter, slot->d_hard, post_out ? slot->d_post : nullptr,
+                                    o.post_kind, slot->d_iters, slot->d_valid);
+                if (r) return r;
+                LDPC_HIP(hipMemcpyAsync(slot->h_hard, slot->d_hard, (size_t)Bc * N, hipMemcpyDeviceToHost, E.stream));
+                if (post_out)
+                    LDPC_HIP(hipMemcpyAsync(slot->h_post, slot->d_post, (size_t)Bc * N * 8, hipMemcpyDeviceToHost,
+                                            E.stream));
+                LDPC_HIP(hipMemcpyAsync(slot->h_iters, slot->d_iters, (size_t)Bc * 4, hipMemcpyDeviceToHost, E.stream));
+                LDPC_HIP(hipMemcpyAsync(slot->h_valid, slot->d_valid, (size_t)Bc, hipMemcpyDeviceToHost, E.stream));
+                LDPC_HIP(hipStreamSynchronize(E.stream));
+                return LDPC_OK;
+            };
+            rc = step();
+            if (rc) break;
+            std::memcpy(hard_out + (size_t)b0 * N, slot->h_hard, (size_t)Bc * N);
+            if (post_out) std::memcpy(post_out + (size_t)b0 * N, slot->h_post, (size_t)Bc * N * 8);
+            if (iters_out) std::memcpy(iters_out + b0, slot->h_iters, (size_t)Bc * 4);
+            if (valid_out) std::memcpy(valid_out + b0, slot->h_valid, (size_t)Bc);
+        }
+        if (rc) { rcs[di] = rc; msgs[di] = ldpc::last_error(); return; }
+        g->give(std::move(slot));
+    };
+    if (devs.size() == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < devs.size(); i++) th.emplace_back(work, i);
+        for (auto& t : th) t.join();
+    }
+    for (size_t i = 0; i < devs.size(); i++)
+        if (rcs[i]) { set_error("device " + std::to_string(devs[i]) + ": " + msgs[i]); return rcs[i]; }
+    return LDPC_OK;
+}
+
+ldpc_engine* ldpc_engine_create(const ldpc_graph* g, int32_t device, int32_t algo, int64_t chunk, int* err)
+{
+    if (!g) { set_error("null graph"); fail(LDPC_ERR_ARG, err); return nullptr; }
+    auto e = std::make_unique<ldpc_engine>();
+    e->e = std::make_unique<Engine>();
+    int rc = e->e->init(&g->h, device, algo, chunk);
+    if (rc) { fail(rc, err); return nullptr; }
+    if (err) *err = LDPC_OK;
+    return e.release();
+}
+
+void ldpc_engine_free(ldpc_engine* e) { delete e; }
+
+int ldpc_engine_decode(ldpc_engine* e, const double* d_in, int32_t in_kind, int64_t B, int32_t max_iter,
+                       uint8_t* d_hard, double* d_post, int32_t post_kind, int32_t* d_iters, uint8_t* d_valid)
+{
+    if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
+    if (B > 0 && !d_in) { set_error("null input"); return LDPC_ERR_ARG; }
+    return e->e->decode(d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
+}
+
+int ldpc_engine_sync(ldpc_engine* e)
+{
+    if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
+    LDPC_HIP(hipSetDevice(e->e->device));
+    LDPC_HIP(hipStreamSynchronize(e->e->stream));
+    return LDPC_OK;
+}
+
+void* ldpc_engine_stream(ldpc_engine* e) { return e ? (void*)e->e->stream : nullptr; }
+
+int ldpc_engine_gen_bsc(ldpc_engine* e, double* d_out, int32_t out_kind, int64_t b0, int64_t B,
+                        const uint8_t* d_codewords, int32_t n_cw, uint64_t seed, double p, double llr_mag)
+{
+    if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
+    return e->e->gen_bsc(d_out, out_kind, b0, B, d_codewords, n_cw, seed, p, llr_mag);
+}
+
+int ldpc_engine_profile(ldpc_engine* e, int32_t enable)
+{
+    if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
+    int rc = e->e->collect_stats();
+    if (rc) return rc;
+    for (int c = 0; c < ldpc::K_NCLASS; c++) { e->e->launches[c] = 0; e->e->ms[c] = 0; }
+    e->e->profile = enable != 0;
+    return LDPC_OK;
+}
+
+int ldpc_engine_stats(ldpc_engine* e, ldpc_kernel_stats* out)
+{
+    if (!e || !out) { set_error("null argument"); return LDPC_ERR_ARG; }
+    int rc = e->e->collect_stats();
+    if (rc) return rc;
+    std::memset(out, 0, sizeof(*out));
+    for (int c = 0; c < ldpc::K_NCLASS; c++) { out->launches[c] = e->e->launches[c]; out->ms[c] = e->e->ms[c]; }
+    return LDPC_OK;
+}
+
+void* ldpc_dev_malloc(int32_t device, size_t bytes)
+{
+    void* p = nullptr;
+    if (hipSetDevice(device) != hipSuccess) { set_error("hipSetDevice failed"); return nullptr; }
+    hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 1));
+    if (e != hipSuccess) { set_error(std::string("hipMalloc: ") + hipGetErrorString(e)); return nullptr; }
+    return p;
+}
+
+int ldpc_dev_free(int32_t device, void* p)
+{
+    LDPC_HIP(hipSetDevice(device));
+    LDPC_HIP(hipFree(p));
+    return LDPC_OK;
+}
+
+int ldpc_dev_memcpy(int32_t device, void* dst, const void* src, size_t bytes, int32_t kind)
+{
+    hipMemcpyKind k = kind == LDPC_H2D ? hipMemcpyHostToDevice : kind == LDPC_D2H ? hipMemcpyDeviceToHost
+                                                                                   : hipMemcpyDeviceToDevice;
+    LDPC_HIP(hipSetDevice(device));
+    LDPC_HIP(hipMemcpy(dst, src, bytes, k));
+    return LDPC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,267 @@
+// engine.hip -- device engine: memory, launch sequence, profiling.
+//
+// One Engine = one device, one HIP stream, message buffers for `cap`
+// resident codewords.  A decode of B codewords runs in passes of <= cap
+// codewords; each pass is the reference's per-frame loop
+// (Run_Belief_Propagation_Decoder dec.cpp:583-605 / Run_MSA_Decoder_INF
+// dec.cpp:1216-1250) executed for all resident codewords at once:
+//
+//   init                                  (Init_*: dec.cpp:608 / 1300)
+//   for n = 0..max_iter:
+//       syndrome(n)  -> codewords with c == 0 or n == max_iter stop
+//       if n == max_iter: break
+//       check phase  (dec.cpp:646-662 / 1398-1433)
+//       variable phase + hard decision (dec.cpp:667-693 / 1597-1678)
+//   finalize (posterior, hard bits, iteration counts)
+//
+// Stopped codewords are masked out of every later kernel (their state stays
+// frozen, exactly as the reference stops touching it), and a tile whose 64
+// codewords have all stopped costs one scalar load per wave.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "engine.hpp"
+#include "kernels.hpp"
+
+namespace ldpc {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+const char* last_error() { return g_err.c_str(); }
+
+int64_t engine_bytes_per_codeword(const HostGraph& g)
+{
+    // v2c + c2v (E fp64 each) + prior (N fp64) + hard (N bits) + state
+    return 2 * g.E * 8 + (int64_t)g.N * 8 + (g.N + 7) / 8 + 8;
+}
+
+Engine::~Engine()
+{
+    if (device >= 0) hipSetDevice(device);
+    if (stream) hipStreamSynchronize(stream);
+    for (int c = 0; c < K_NCLASS; c++)
+        for (auto& p : ev_live[c]) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
+    for (auto e : ev_pool) hipEventDestroy(e);
+    hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge);
+    hipFree(v2c); hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
+    if (stream) hipStreamDestroy(stream);
+}
+
+template <typename T>
+static int upload(T** dst, const std::vector<T>& v)
+{
+    const size_t n = std::max<size_t>(v.size(), 1);
+    LDPC_HIP(hipMalloc((void**)dst, n * sizeof(T)));
+    if (!v.empty()) LDPC_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return LDPC_OK;
+}
+
+int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk)
+{
+    g = graph;
+    device = dev;
+    algo = algorithm;
+    if (algo != LDPC_ALGO_BP && algo != LDPC_ALGO_MSA) { set_error("unknown algorithm"); return LDPC_ERR_ARG; }
+    int ndev = 0;
+    LDPC_HIP(hipGetDeviceCount(&ndev));
+    if (dev < 0 || dev >= ndev) { set_error("device ordinal out of range"); return LDPC_ERR_DEVICE; }
+    LDPC_HIP(hipSetDevice(dev));
+    LDPC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+
+    if (chunk <= 0) {
+        size_t fr = 0, tot = 0;
+        LDPC_HIP(hipMemGetInfo(&fr, &tot));
+        // half of the free memory for the resident state, at most 16384 codewords
+        chunk = std::min<int64_t>(16384, (int64_t)(fr / 2) / engine_bytes_per_codeword(*g));
+    }
+    cap = std::max<int64_t>(64, (chunk + 63) / 64 * 64);
+    cap_tiles = cap / 64;
+    if (cap_tiles > 65535) { set_error("chunk too large (max 4194240 codewords)"); return LDPC_ERR_ARG; }
+
+    int rc;
+    if ((rc = upload(&d_row_ptr, g->row_ptr)) || (rc = upload(&d_col_idx, g->col_idx)) ||
+        (rc = upload(&d_col_ptr, g->col_ptr)) || (rc = upload(&d_col_edge, g->col_edge)))
+        return rc;
+    if (g->regular_dc && g->dc_max > 0) {
+        std::vector<int32_t> T((size_t)g->dc_max * g->M);
+        for (int32_t i = 0; i < g->M; i++)
+            for (int k = 0; k < g->dc_max; k++) T[(size_t)k * g->M + i] = g->col_idx[(size_t)i * g->dc_max + k];
+        if ((rc = upload(&d_col_idx_T, T))) return rc;
+    }
+    const size_t E = (size_t)std::max<int64_t>(g->E, 1);
+    LDPC_HIP(hipMalloc((void**)&v2c, (size_t)cap * E * sizeof(double)));
+    LDPC_HIP(hipMalloc((void**)&c2v, (size_t)cap * E * sizeof(double)));
+    LDPC_HIP(hipMalloc((void**)&prior, (size_t)cap * g->N * sizeof(double)));
+    LDPC_HIP(hipMalloc((void**)&hard, (size_t)cap_tiles * g->N * sizeof(uint64_t)));
+    LDPC_HIP(hipMalloc((void**)&active, (size_t)cap_tiles * sizeof(uint64_t)));
+    LDPC_HIP(hipMalloc((void**)&iters, (size_t)cap * sizeof(int32_t)));
+    LDPC_HIP(hipMalloc((void**)&valid, (size_t)cap * sizeof(uint8_t)));
+    return LDPC_OK;
+}
+
+hipEvent_t Engine::get_event()
+{
+    if (!ev_pool.empty()) { hipEvent_t e = ev_pool.back(); ev_pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int Engine::mark_begin(KClass c, hipEvent_t* b)
+{
+    launches[c]++;
+    *b = nullptr;
+    if (!profile) return LDPC_OK;
+    *b = get_event();
+    if (!*b) { set_error("hipEventCreate failed"); return LDPC_ERR_DEVICE; }
+    LDPC_HIP(hipEventRecord(*b, stream));
+    return LDPC_OK;
+}
+
+int Engine::mark_end(KClass c, hipEvent_t b)
+{
+    LDPC_HIP(hipGetLastError());
+    if (!profile || !b) return LDPC_OK;
+    hipEvent_t e = get_event();
+    if (!e) { set_error("hipEventCreate failed"); return LDPC_ERR_DEVICE; }
+    LDPC_HIP(hipEventRecord(e, stream));
+    ev_live[c].push_back({b, e});
+    return LDPC_OK;
+}
+
+int Engine::collect_stats()
+{
+    LDPC_HIP(hipSetDevice(device));
+    LDPC_HIP(hipStreamSynchronize(stream));
+    for (int c = 0; c < K_NCLASS; c++) {
+        for (auto& p : ev_live[c]) {
+            float t = 0.f;
+            LDPC_HIP(hipEventElapsedTime(&t, p.first, p.second));
+            ms[c] += t;
+            ev_pool.push_back(p.first);
+            ev_pool.push_back(p.second);
+        }
+        ev_live[c].clear();
+    }
+    return LDPC_OK;
+}
+
+#define LAUNCH(cls, ...)                                  \
+    do {                                                  \
+        hipEvent_t _b;                                    \
+        int _rc = mark_begin(cls, &_b);                   \
+        if (_rc) return _rc;                              \
+        __VA_ARGS__;                                      \
+        _rc = mark_end(cls, _b);                          \
+        if (_rc) return _rc;                              \
+    } while (0)
+
+int Engine::run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_iter, uint8_t* d_hard,
+                      double* d_post, int post_kind, int32_t* d_iters, uint8_t* d_valid)
+{
+    using namespace dev;
+    const int32_t M = g->M, N = g->N;
+    const int64_t E = g->E;
+    const int64_t tiles = (Bc + 63) / 64;
+    const int msa = algo == LDPC_ALGO_MSA;
+    if (msa && in_kind == LDPC_IN_LR) { set_error("min-sum takes LLR input"); return LDPC_ERR_ARG; }
+    if (msa && post_kind == LDPC_POST_RATIO) { set_error("LDPC_POST_RATIO is BP-only"); return LDPC_ERR_ARG; }
+    const bool reg_row72 = g->regular_dc && g->dc_max == 72;
+    const bool reg_col8 = g->regular_dv && g->dv_max == 8;
+    const bool reg_rowT = g->regular_dc && d_col_idx_T != nullptr;
+
+    const dim3 blk(256);
+    const dim3 g_init((N + 63) / 64, (unsigned)tiles);
+    const dim3 g_rows((M + 3) / 4, (unsigned)tiles);
+    const dim3 g_cols((N + 3) / 4, (unsigned)tiles);
+
+    LAUNCH(K_INIT, hipLaunchKernelGGL(k_init, g_init, blk, 0, stream, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, msa, Bc, N,
+                                      E, d_col_ptr, d_col_edge, prior, v2c, hard, active, iters, valid));
+    for (int32_t n = 0;; n++) {
+        if (reg_rowT && g->dc_max == 72)
+            LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome<72>, dim3((unsigned)tiles), dim3(1024), 0, stream, hard, active,
+                                             iters, valid, d_row_ptr, d_col_idx, d_col_idx_T, M, N, n, max_iter));
+        else
+            LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome<0>, dim3((unsigned)tiles), dim3(1024), 0, stream, hard, active,
+                                             iters, valid, d_row_ptr, d_col_idx, d_col_idx_T, M, N, n, max_iter));
+        if (n >= max_iter) break;
+        if (!msa) {
+            if (reg_row72)
+                LAUNCH(K_CHECK, hipLaunchKernelGGL(k_check_bp<72>, g_rows, blk, 0, stream, v2c, c2v, active, M, E));
+            else
+                LAUNCH(K_CHECK, hipLaunchKernelGGL(k_check_bp_gen, g_rows, blk, 0, stream, v2c, c2v, active, d_row_ptr,
+                                                   M, E));
+            if (reg_col8)
+                LAUNCH(K_VAR, hipLaunchKernelGGL(k_var_bp<8>, g_cols, blk, 0, stream, c2v, v2c, prior, hard, active,
+                                                 d_col_edge, N, E));
+            else
+                LAUNCH(K_VAR, hipLaunchKernelGGL(k_var_bp_gen, g_cols, blk, 0, stream, c2v, v2c, prior, hard, active,
+                                                 d_col_ptr, d_col_edge, N, E));
+        } else {
+            if (reg_row72)
+                LAUNCH(K_CHECK, hipLaunchKernelGGL(k_check_msa<72>, g_rows, blk, 0, stream, v2c, c2v, active, M, E));
+            else
+                LAUNCH(K_CHECK, hipLaunchKernelGGL(k_check_msa_gen, g_rows, blk, 0, stream, v2c, c2v, active,
+                                                   d_row_ptr, M, E));
+            if (reg_col8)
+                LAUNCH(K_VAR, hipLaunchKernelGGL(k_var_msa<8>, g_cols, blk, 0, stream, c2v, v2c, prior, hard, active,
+                                                 d_col_edge, N, E));
+            else
+                LAUNCH(K_VAR, hipLaunchKernelGGL(k_var_msa_gen, g_cols, blk, 0, stream, c2v, v2c, prior, hard, active,
+                                                 d_col_ptr, d_col_edge, N, E));
+        }
+    }
+    if (d_post)
+        LAUNCH(K_FINAL, hipLaunchKernelGGL(k_finalize, g_cols, blk, 0, stream, c2v, prior, iters, d_col_ptr, d_col_edge,
+                                           d_post, msa, post_kind == LDPC_POST_RATIO ? 1 : 0, Bc, N, E));
+    if (d_hard) {
+        const int64_t nblk = Bc * ((N + 255) / 256);
+        const unsigned grid = (unsigned)std::min<int64_t>(nblk, 1 << 20);
+        LAUNCH(K_FINAL, hipLaunchKernelGGL(k_unpack_hard, dim3(grid), blk, 0, stream, hard, d_hard, Bc, N));
+    }
+    if (d_iters) LDPC_HIP(hipMemcpyAsync(d_iters, iters, (size_t)Bc * sizeof(int32_t), hipMemcpyDeviceToDevice, stream));
+    if (d_valid) LDPC_HIP(hipMemcpyAsync(d_valid, valid, (size_t)Bc, hipMemcpyDeviceToDevice, stream));
+    return LDPC_OK;
+}
+
+int Engine::decode(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
+                   int post_kind, int32_t* d_iters, uint8_t* d_valid)
+{
+    if (B < 0 || max_iter < 0) { set_error("B and max_iter must be >= 0"); return LDPC_ERR_ARG; }
+    if (B == 0) return LDPC_OK;
+    LDPC_HIP(hipSetDevice(device));
+    // balanced passes of <= cap codewords (multiples of 64 except the tail)
+    const int64_t npass = (B + cap - 1) / cap;
+    const int64_t per = std::min<int64_t>(cap, ((B + npass - 1) / npass + 63) / 64 * 64);
+    const size_t N = (size_t)g->N;
+    for (int64_t b0 = 0; b0 < B; b0 += per) {
+        const int64_t Bc = std::min<int64_t>(per, B - b0);
+        int rc = run_chunk(d_in + (size_t)b0 * N, in_kind, Bc, max_iter, d_hard ? d_hard + (size_t)b0 * N : nullptr,
+                           d_post ? d_post + (size_t)b0 * N : nullptr, post_kind, d_iters ? d_iters + b0 : nullptr,
+                           d_valid ? d_valid + b0 : nullptr);
+        if (rc) return rc;
+    }
+    return LDPC_OK;
+}
+
+int Engine::gen_bsc(double* d_out, int out_kind, int64_t b0, int64_t B, const uint8_t* d_cw, int32_t n_cw,
+                    uint64_t seed, double p, double llr_mag)
+{
+    if (B <= 0) return LDPC_OK;
+    if (n_cw <= 0 || !d_cw || !d_out) { set_error("gen_bsc: bad arguments"); return LDPC_ERR_ARG; }
+    LDPC_HIP(hipSetDevice(device));
+    double pos = llr_mag, neg = -llr_mag;
+    if (out_kind == LDPC_IN_LR) {  // the reference's host exp (DNA_main.cpp:1344)
+        pos = std::exp(llr_mag);
+        neg = std::exp(-llr_mag);
+    }
+    const uint64_t seedmix = dev::splitmix64(seed);
+    LAUNCH(K_OTHER, hipLaunchKernelGGL(dev::k_gen_bsc, dim3(8192), dim3(256), 0, stream, d_out,
+                                       out_kind == LDPC_IN_LR ? 1 : 0, b0, B, d_cw, n_cw, g->N, seedmix, p, pos, neg));
+    return LDPC_OK;
+}
+
+}  // namespace ldpc

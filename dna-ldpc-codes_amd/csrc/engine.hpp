@@ -1,0 +1,79 @@
+// engine.hpp -- internal interface between the C ABI and the HIP engine.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ldpc_amd.h"
+#include "graph.hpp"
+
+namespace ldpc {
+
+// thread-local error string behind ldpc_last_error()
+void set_error(const std::string& msg);
+const char* last_error();
+
+#define LDPC_HIP(call)                                                                           \
+    do {                                                                                         \
+        hipError_t _e = (call);                                                                  \
+        if (_e != hipSuccess) {                                                                  \
+            ::ldpc::set_error(std::string(#call) + ": " + hipGetErrorString(_e));                \
+            return LDPC_ERR_DEVICE;                                                              \
+        }                                                                                        \
+    } while (0)
+
+enum KClass { K_CHECK = 0, K_VAR = 1, K_SYN = 2, K_INIT = 3, K_FINAL = 4, K_OTHER = 5, K_NCLASS = 6 };
+
+struct Engine {
+    const HostGraph* g = nullptr;
+    int device = 0;
+    int algo = LDPC_ALGO_BP;
+    hipStream_t stream = nullptr;
+    int64_t cap = 0;        // codewords per pass (multiple of 64)
+    int64_t cap_tiles = 0;
+    // graph on device
+    int32_t* d_row_ptr = nullptr;
+    int32_t* d_col_idx = nullptr;
+    int32_t* d_col_idx_T = nullptr;  // [dc][M] for regular rows (syndrome gathers)
+    int32_t* d_col_ptr = nullptr;
+    int32_t* d_col_edge = nullptr;
+    // decoder state
+    double* v2c = nullptr;
+    double* c2v = nullptr;
+    double* prior = nullptr;
+    uint64_t* hard = nullptr;
+    uint64_t* active = nullptr;
+    int32_t* iters = nullptr;
+    uint8_t* valid = nullptr;
+    // profiling
+    bool profile = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_live[K_NCLASS];
+    std::vector<hipEvent_t> ev_pool;
+    int64_t launches[K_NCLASS] = {0};
+    double ms[K_NCLASS] = {0};
+
+    ~Engine();
+    int init(const HostGraph* graph, int dev, int algorithm, int64_t chunk);
+    // decode Bc <= cap codewords whose [Bc][N] input is at d_in (device)
+    int run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_iter, uint8_t* d_hard, double* d_post,
+                  int post_kind, int32_t* d_iters, uint8_t* d_valid);
+    int decode(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
+               int post_kind, int32_t* d_iters, uint8_t* d_valid);
+    int gen_bsc(double* d_out, int out_kind, int64_t b0, int64_t B, const uint8_t* d_cw, int32_t n_cw, uint64_t seed,
+                double p, double llr_mag);
+    int collect_stats();
+
+  private:
+    hipEvent_t get_event();
+    int mark_begin(KClass c, hipEvent_t* b);
+    int mark_end(KClass c, hipEvent_t b);
+};
+
+// bytes of device memory per resident codeword
+int64_t engine_bytes_per_codeword(const HostGraph& g);
+
+}  // namespace ldpc

@@ -1,0 +1,602 @@
+// kernels.hpp -- HIP device kernels for batched LDPC decoding on MI355X (gfx950).
+//
+// Layout in HBM (one engine = one chunk of C codewords, C a multiple of 64):
+//   tile t = 64 consecutive codewords; lane l of a wavefront = codeword 64t+l.
+//   v2c [t][E][64] fp64  BP: d = 1 - 2/(1+pr) of the variable->check message
+//                        MSA: msg_v_to_c_fp
+//   c2v [t][E][64] fp64  BP: lr (check->variable likelihood ratio)
+//                        MSA: msg_c_to_v_fp
+//   prior [t][N][64] fp64  BP: LR = exp(LLR);  MSA: LLR
+//   hard [t][N] u64     bit l = hard decision of codeword 64t+l (a ballot)
+//   active [t] u64      bit l = codeword 64t+l still iterating
+// Every message access of a wave is one 512-B contiguous segment (64 lanes x
+// 8 B) in BOTH phases, and the graph indices (CSR row offsets, CSC edge ids)
+// are wave-uniform scalar loads.  Each lane runs the reference's sequential
+// per-row / per-column loops, which is what bit-exactness with the
+// reference's fp64 operation order requires (no tree reductions of the
+// products/sums; only the order-free XOR/OR syndrome uses cross-lane ops).
+//
+// Compiled with -ffp-contract=off and without fast-math: fp64 '/' lowers to
+// the correctly-rounded IEEE division, no FMA contraction, isnan() honoured.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace ldpc {
+namespace dev {
+
+constexpr int TILE = 64;
+
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m)
+{
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo = (uint32_t)__shfl_xor((int)lo, m);
+    hi = (uint32_t)__shfl_xor((int)hi, m);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// ---------------------------------------------------------------------------
+// init: transpose a [b][N] input chunk into the tiled layout, set the initial
+// messages and hard decisions.
+//   BP  : Init_Belief_Propagation dec.cpp:608-629  (pr = LR, lr = 1, dblk = LR < 1);
+//         d = 1 - 2/(1+pr) is what the check phase consumes (dec.cpp:652,660).
+//   MSA : Init_MSA_INF dec.cpp:1300-1329 (v2c = LLR, dblk = !(LLR > 0)).
+// grid (ceil(N/64), tiles), block 256; LDS 64x65 fp64 transpose tile.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_init(const double* __restrict__ in, int in_is_llr, int algo_msa,
+                                              int64_t Bc, int32_t N, int64_t E,
+                                              const int32_t* __restrict__ col_ptr, const int32_t* __restrict__ col_edge,
+                                              double* __restrict__ prior, double* __restrict__ v2c,
+                                              uint64_t* __restrict__ hard, uint64_t* __restrict__ active,
+                                              int32_t* __restrict__ iters, uint8_t* __restrict__ valid)
+{
+    __shared__ double s[TILE][TILE + 1];
+    const int lane = lane_id(), w = wave_id();
+    const int64_t t = blockIdx.y;
+    const int32_t j0 = blockIdx.x * TILE;
+    for (int r = w; r < TILE; r += 4) {
+        const int64_t b = t * TILE + r;
+        const int32_t j = j0 + lane;
+        double v = in_is_llr ? 0.0 : 1.0;  // pad lanes: LLR 0 / LR 1 (never active)
+        if (b < Bc && j < N) v = in[(size_t)b * N + j];
+        s[r][lane] = v;
+    }
+    __syncthreads();
+    const int64_t b = t * TILE + lane;
+    const bool inb = b < Bc;
+    for (int c = w; c < TILE; c += 4) {
+        const int32_t j = j0 + c;
+        if (j >= N) break;
+        const double x = s[lane][c];
+        double pv, m;
+        bool h;
+        if (algo_msa) {
+            pv = x;  // LLR
+            m = x;
+            h = !(x > 0);
+        } else {
+            pv = in_is_llr ? exp(x) : x;  // LR (ocml exp when the input is LLR)
+            m = 1.0 - 2.0 / (1.0 + pv);
+            h = (pv < 1.0);
+        }
+        prior[((size_t)t * N + j) * TILE + lane] = pv;
+        const int32_t a = col_ptr[j], e1 = col_ptr[j + 1];
+        for (int32_t q = a; q < e1; ++q) v2c[((size_t)t * E + col_edge[q]) * TILE + lane] = m;
+        const uint64_t hm = __ballot(h && inb);
+        if (lane == 0) hard[(size_t)t * N + j] = hm;
+    }
+    if (blockIdx.x == 0 && w == 0) {
+        const uint64_t am = __ballot(inb);
+        if (lane == 0) active[t] = am;
+        if (inb) { iters[b] = 0; valid[b] = 0; }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// syndrome + termination bookkeeping for iteration n (one block per tile).
+// check() check.cpp:28-45 / mod2sparse_mulvec mod2sparse.cpp:855-881 on the
+// 64 codewords of the tile at once: row parity = XOR of the column ballots.
+// Run_*_Decoder loop control dec.cpp:594-599 / 1223-1246:
+//   c == 0            -> stop, iters = n, valid = 1
+//   n == max_iter     -> stop, iters = n, valid = (c == 0)
+// ---------------------------------------------------------------------------
+template <int DC>
+__global__ __launch_bounds__(1024) void k_syndrome(const uint64_t* __restrict__ hard, uint64_t* __restrict__ active,
+                                                   int32_t* __restrict__ iters, uint8_t* __restrict__ valid,
+                                                   const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col_idx,
+                                                   const int32_t* __restrict__ col_idx_T, int32_t M, int32_t N,
+                                                   int32_t n, int32_t max_iter)
+{
+    __shared__ uint64_t red[16];
+    const int64_t t = blockIdx.x;
+    const uint64_t act = active[t];
+    if (act == 0) return;
+    const uint64_t* h = hard + (size_t)t * N;
+    uint64_t u = 0;
+    for (int32_t i = threadIdx.x; i < M; i += blockDim.x) {
+        uint64_t p = 0;
+        if (DC > 0) {
+#pragma unroll 24
+            for (int k = 0; k < DC; ++k) p ^= h[col_idx_T[(size_t)k * M + i]];
+        } else {
+            for (int32_t e = row_ptr[i]; e < row_ptr[i + 1]; ++e) p ^= h[col_idx[e]];
+        }
+        u |= p;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) u |= shfl_xor_u64(u, off);
+    const int lane = lane_id(), w = wave_id();
+    if (lane == 0) red[w] = u;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint64_t U = 0;
+        const int nw = blockDim.x >> 6;
+        for (int q = 0; q < nw; ++q) U |= red[q];
+        if ((act >> lane) & 1ull) {
+            const size_t b = (size_t)t * TILE + lane;
+            if (!((U >> lane) & 1ull)) { iters[b] = n; valid[b] = 1; }
+            else if (n == max_iter) { iters[b] = n; valid[b] = 0; }
+        }
+        if (lane == 0) active[t] = (n == max_iter) ? 0ull : (act & U);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// BP check-node phase, regular row degree DC (Iter_Belief_Propagation
+// dec.cpp:646-662).  Per row and lane:
+//   forward  lr_k <- p_k = (((1*d_0)*d_1)*...)*d_{k-1}
+//   backward s = 1; for k = DC-1..0: t = p_k*s; lr_k = (1+t)/(1-t); s *= d_k
+// d_k (= 1 - 2/(1+pr_k), stored by the variable phase) stays in registers;
+// the prefix products are kept as checkpoints every SEG edges and recomputed
+// segment by segment in the backward pass (same operations in the same order
+// -> identical values), which keeps the kernel at 2 waves/SIMD.
+// grid (ceil(M/4), tiles), block 256: one wave per (row, tile).
+// ---------------------------------------------------------------------------
+template <int DC>
+__global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ dmsg, double* __restrict__ lr,
+                                                  const uint64_t* __restrict__ active, int32_t M, int64_t E)
+{
+    constexpr int SEG = 8;
+    constexpr int NSEG = (DC + SEG - 1) / SEG;
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = blockIdx.y;
+    if (row >= M) return;
+    const uint64_t act = active[t];
+    if (!((act >> lane) & 1ull)) return;
+    const size_t base = ((size_t)t * E + (size_t)row * DC) * TILE + lane;
+    const double* __restrict__ src = dmsg + base;
+    double* __restrict__ dst = lr + base;
+
+    double x[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) x[k] = src[(size_t)k * TILE];
+
+    double cp[NSEG];
+    double p = 1.0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        if (k % SEG == 0) cp[k / SEG] = p;
+        p = p * x[k];
+    }
+    double s = 1.0;
+#pragma unroll
+    for (int g = NSEG - 1; g >= 0; --g) {
+        double pk[SEG];
+        double q = cp[g];
+        // opaque copy: stops the compiler from CSE-ing the recomputed prefixes
+        // with the forward pass (which would keep all DC prefixes live)
+        asm volatile("" : "+v"(q));
+#pragma unroll
+        for (int i = 0; i < SEG; ++i) {
+            const int k = g * SEG + i;
+            if (k < DC) { pk[i] = q; q = q * x[k]; }
+        }
+#pragma unroll
+        for (int i = SEG - 1; i >= 0; --i) {
+            const int k = g * SEG + i;
+            if (k < DC) {
+                const double tt = pk[i] * s;
+                dst[(size_t)k * TILE] = (1.0 + tt) / (1.0 - tt);
+                s = s * x[k];
+            }
+        }
+    }
+}
+
+// Generic row degree: the prefix products go through the lr array exactly as
+// the reference does (e->lr = dl in the forward pass, dec.cpp:650-653).
+__global__ __launch_bounds__(256) void k_check_bp_gen(const double* __restrict__ dmsg, double* __restrict__ lr,
+                                                      const uint64_t* __restrict__ active,
+                                                      const int32_t* __restrict__ row_ptr, int32_t M, int64_t E)
+{
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = blockIdx.y;
+    if (row >= M) return;
+    const uint64_t act = active[t];
+    if (!((act >> lane) & 1ull)) return;
+    const int32_t a = row_ptr[row], b = row_ptr[row + 1];
+    const size_t tb = (size_t)t * E;
+    double dl = 1.0;
+    for (int32_t e = a; e < b; ++e) {
+        const size_t o = (tb + e) * TILE + lane;
+        lr[o] = dl;
+        dl = dl * dmsg[o];
+    }
+    dl = 1.0;
+    for (int32_t e = b - 1; e >= a; --e) {
+        const size_t o = (tb + e) * TILE + lane;
+        const double tt = lr[o] * dl;
+        lr[o] = (1.0 + tt) / (1.0 - tt);
+        dl = dl * dmsg[o];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// BP variable-node phase, regular column degree DV (dec.cpp:667-693):
+//   forward  pr_s = P_s; P_{s+1} = P_s * lr_s; P_0 = LR
+//   P = P_DV; NaN -> 1; dblk = (P <= 1)
+//   backward acc = 1; s = DV-1..0: pr_s *= acc; NaN -> 1; acc *= lr_s
+// then stores d_s = 1 - 2/(1+pr_s) for the next check phase and the ballot of
+// the hard decisions.  Converged lanes keep their state untouched.
+// grid (ceil(N/4), tiles), block 256: one wave per (column, tile).
+// ---------------------------------------------------------------------------
+template <int DV>
+__global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, double* __restrict__ dmsg,
+                                                const double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                                const uint64_t* __restrict__ active, const int32_t* __restrict__ col_edge,
+                                                int32_t N, int64_t E)
+{
+    const int lane = lane_id();
+    const int32_t j = blockIdx.x * 4 + wave_id();
+    const int64_t t = blockIdx.y;
+    if (j >= N) return;
+    const uint64_t act = active[t];
+    if (act == 0) return;
+    const bool live = (act >> lane) & 1ull;
+    int32_t eid[DV];
+#pragma unroll
+    for (int s = 0; s < DV; ++s) eid[s] = col_edge[(size_t)j * DV + s];
+    const size_t tb = (size_t)t * E;
+    bool h = false;
+    if (live) {
+        const double LR = prior[((size_t)t * N + j) * TILE + lane];
+        double l[DV], pr[DV];
+#pragma unroll
+        for (int s = 0; s < DV; ++s) l[s] = lr[(tb + eid[s]) * TILE + lane];
+        double p = LR;
+#pragma unroll
+        for (int s = 0; s < DV; ++s) { pr[s] = p; p = p * l[s]; }
+        if (__builtin_isnan(p)) p = 1.0;
+        h = (p <= 1.0);
+        double acc = 1.0;
+#pragma unroll
+        for (int s = DV - 1; s >= 0; --s) {
+            double v = pr[s] * acc;
+            if (__builtin_isnan(v)) v = 1.0;
+            acc = acc * l[s];
+            dmsg[(tb + eid[s]) * TILE + lane] = 1.0 - 2.0 / (1.0 + v);
+        }
+    }
+    const uint64_t m = __ballot(h);
+    if (lane == 0) {
+        const size_t o = (size_t)t * N + j;
+        const uint64_t old = (act == ~0ull) ? 0ull : hard[o];
+        hard[o] = (old & ~act) | (m & act);
+    }
+}
+
+// Generic column degree: the partial products go through the v2c array
+// exactly as the reference keeps them in e->pr.
+__global__ __launch_bounds__(256) void k_var_bp_gen(const double* __restrict__ lr, double* __restrict__ dmsg,
+                                                    const double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                                    const uint64_t* __restrict__ active, const int32_t* __restrict__ col_ptr,
+                                                    const int32_t* __restrict__ col_edge, int32_t N, int64_t E)
+{
+    const int lane = lane_id();
+    const int32_t j = blockIdx.x * 4 + wave_id();
+    const int64_t t = blockIdx.y;
+    if (j >= N) return;
+    const uint64_t act = active[t];
+    if (act == 0) return;
+    const bool live = (act >> lane) & 1ull;
+    const int32_t a = col_ptr[j], b = col_ptr[j + 1];
+    const size_t tb = (size_t)t * E;
+    bool h = false;
+    if (live) {
+        double p = prior[((size_t)t * N + j) * TILE + lane];
+        for (int32_t q = a; q < b; ++q) {
+            const size_t o = (tb + col_edge[q]) * TILE + lane;
+            dmsg[o] = p;
+            p = p * lr[o];
+        }
+        if (__builtin_isnan(p)) p = 1.0;
+        h = (p <= 1.0);
+        double acc = 1.0;
+        for (int32_t q = b - 1; q >= a; --q) {
+            const size_t o = (tb + col_edge[q]) * TILE + lane;
+            double v = dmsg[o] * acc;
+            if (__builtin_isnan(v)) v = 1.0;
+            acc = acc * lr[o];
+            dmsg[o] = 1.0 - 2.0 / (1.0 + v);
+        }
+    }
+    const uint64_t m = __ballot(h);
+    if (lane == 0) {
+        const size_t o = (size_t)t * N + j;
+        const uint64_t old = (act == ~0ull) ? 0ull : hard[o];
+        hard[o] = (old & ~act) | (m & act);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Min-sum check-node phase (Check_Update_MSA_INF dec.cpp:1398-1433) in O(dc):
+// for edge k the reference scans the other edges o in order with
+//   if (mag == -1 || mag > |x_o|) mag = |x_o|;   sign *= (x_o >= 0 ? 1 : -1)
+// which equals: |x_f| if it is NaN (f = first other edge: 1 for k = 0, else 0
+// -- a NaN first value sticks because every later comparison is false),
+// otherwise the minimum over the non-NaN others = (k == argmin ? min2 : min1)
+// with argmin the FIRST index of the minimum.  sign = product over others of
+// (x >= 0 ? +1 : -1) (NaN counts -1).  c2v = (double)sign * mag.
+// dc == 1: mag stays -1 -> 0, sign 1 -> 0.0 (dec.cpp:1427-1430).
+// ---------------------------------------------------------------------------
+template <int DC>
+__global__ __launch_bounds__(256) void k_check_msa(const double* __restrict__ v2c, double* __restrict__ c2v,
+                                                   const uint64_t* __restrict__ active, int32_t M, int64_t E)
+{
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = blockIdx.y;
+    if (row >= M) return;
+    const uint64_t act = active[t];
+    if (!((act >> lane) & 1ull)) return;
+    const size_t base = ((size_t)t * E + (size_t)row * DC) * TILE + lane;
+    const double* __restrict__ src = v2c + base;
+    double* __restrict__ dst = c2v + base;
+    double x[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) x[k] = src[(size_t)k * TILE];
+    if (DC == 1) {
+        dst[0] = 0.0;
+        return;
+    }
+    double m1 = __builtin_inf(), m2 = __builtin_inf();
+    int i1 = -1;
+    uint32_t neg = 0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const double a = __builtin_fabs(x[k]);
+        neg ^= (x[k] >= 0) ? 0u : 1u;
+        if (a < m1) { m1 = a; i1 = k; }  // NaN never compares less; first index kept
+    }
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const double a = __builtin_fabs(x[k]);
+        if (k != i1 && a < m2) m2 = a;
+    }
+    const double a0 = __builtin_fabs(x[0]), a1 = __builtin_fabs(x[DC > 1 ? 1 : 0]);
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const double af = (k == 0) ? a1 : a0;
+        double mag = (k == i1) ? m2 : m1;
+        if (__builtin_isnan(af)) mag = af;
+        const uint32_t nk = (x[k] >= 0) ? 0u : 1u;
+        const int sign = ((neg ^ nk) & 1u) ? -1 : 1;
+        dst[(size_t)k * TILE] = (double)sign * mag;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_check_msa_gen(const double* __restrict__ v2c, double* __restrict__ c2v,
+                                                       const uint64_t* __restrict__ active,
+                                                       const int32_t* __restrict__ row_ptr, int32_t M, int64_t E)
+{
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = blockIdx.y;
+    if (row >= M) return;
+    const uint64_t act = active[t];
+    if (!((act >> lane) & 1ull)) return;
+    const int32_t a = row_ptr[row], b = row_ptr[row + 1];
+    const size_t tb = (size_t)t * E;
+    if (b - a == 0) return;
+    if (b - a == 1) { c2v[(tb + a) * TILE + lane] = 0.0; return; }
+    double m1 = __builtin_inf(), m2 = __builtin_inf();
+    int32_t i1 = -1;
+    uint32_t neg = 0;
+    for (int32_t e = a; e < b; ++e) {
+        const double xv = v2c[(tb + e) * TILE + lane];
+        const double av = __builtin_fabs(xv);
+        neg ^= (xv >= 0) ? 0u : 1u;
+        if (av < m1) { m1 = av; i1 = e; }
+    }
+    for (int32_t e = a; e < b; ++e) {
+        const double av = __builtin_fabs(v2c[(tb + e) * TILE + lane]);
+        if (e != i1 && av < m2) m2 = av;
+    }
+    const double a0 = __builtin_fabs(v2c[(tb + a) * TILE + lane]);
+    const double a1 = __builtin_fabs(v2c[(tb + a + 1) * TILE + lane]);
+    for (int32_t e = a; e < b; ++e) {
+        const size_t o = (tb + e) * TILE + lane;
+        const double xv = v2c[o];
+        const double af = (e == a) ? a1 : a0;
+        double mag = (e == i1) ? m2 : m1;
+        if (__builtin_isnan(af)) mag = af;
+        const uint32_t nk = (xv >= 0) ? 0u : 1u;
+        const int sign = ((neg ^ nk) & 1u) ? -1 : 1;
+        c2v[o] = (double)sign * mag;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Min-sum variable-node phase + decision (Variable_Update_MSA_INF
+// dec.cpp:1597-1619, Decision_MSA_INF dec.cpp:1659-1678):
+//   v2c_s = ((LLR + c_0) + c_1) ... skipping c_s, ascending row order
+//   L = LLR + c_0 + ... + c_{DV-1};  dblk = !(L > 0)
+// ---------------------------------------------------------------------------
+template <int DV>
+__global__ __launch_bounds__(256) void k_var_msa(const double* __restrict__ c2v, double* __restrict__ v2c,
+                                                 const double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                                 const uint64_t* __restrict__ active, const int32_t* __restrict__ col_edge,
+                                                 int32_t N, int64_t E)
+{
+    const int lane = lane_id();
+    const int32_t j = blockIdx.x * 4 + wave_id();
+    const int64_t t = blockIdx.y;
+    if (j >= N) return;
+    const uint64_t act = active[t];
+    if (act == 0) return;
+    const bool live = (act >> lane) & 1ull;
+    int32_t eid[DV];
+#pragma unroll
+    for (int s = 0; s < DV; ++s) eid[s] = col_edge[(size_t)j * DV + s];
+    const size_t tb = (size_t)t * E;
+    bool h = false;
+    if (live) {
+        const double llr = prior[((size_t)t * N + j) * TILE + lane];
+        double c[DV];
+#pragma unroll
+        for (int s = 0; s < DV; ++s) c[s] = c2v[(tb + eid[s]) * TILE + lane];
+#pragma unroll
+        for (int s = 0; s < DV; ++s) {
+            double sum = llr;
+#pragma unroll
+            for (int r = 0; r < DV; ++r)
+                if (r != s) sum = sum + c[r];
+            v2c[(tb + eid[s]) * TILE + lane] = sum;
+        }
+        double L = llr;
+#pragma unroll
+        for (int s = 0; s < DV; ++s) L = L + c[s];
+        h = !(L > 0);
+    }
+    const uint64_t m = __ballot(h);
+    if (lane == 0) {
+        const size_t o = (size_t)t * N + j;
+        const uint64_t old = (act == ~0ull) ? 0ull : hard[o];
+        hard[o] = (old & ~act) | (m & act);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ c2v, double* __restrict__ v2c,
+                                                     const double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                                     const uint64_t* __restrict__ active, const int32_t* __restrict__ col_ptr,
+                                                     const int32_t* __restrict__ col_edge, int32_t N, int64_t E)
+{
+    const int lane = lane_id();
+    const int32_t j = blockIdx.x * 4 + wave_id();
+    const int64_t t = blockIdx.y;
+    if (j >= N) return;
+    const uint64_t act = active[t];
+    if (act == 0) return;
+    const bool live = (act >> lane) & 1ull;
+    const int32_t a = col_ptr[j], b = col_ptr[j + 1];
+    const size_t tb = (size_t)t * E;
+    bool h = false;
+    if (live) {
+        const double llr = prior[((size_t)t * N + j) * TILE + lane];
+        // v2c is written only after all sums are formed, c2v is read-only here
+        for (int32_t s = a; s < b; ++s) {
+            double sum = llr;
+            for (int32_t r = a; r < b; ++r)
+                if (r != s) sum = sum + c2v[(tb + col_edge[r]) * TILE + lane];
+            v2c[(tb + col_edge[s]) * TILE + lane] = sum;
+        }
+        double L = llr;
+        for (int32_t s = a; s < b; ++s) L = L + c2v[(tb + col_edge[s]) * TILE + lane];
+        h = !(L > 0);
+    }
+    const uint64_t m = __ballot(h);
+    if (lane == 0) {
+        const size_t o = (size_t)t * N + j;
+        const uint64_t old = (act == ~0ull) ? 0ull : hard[o];
+        hard[o] = (old & ~act) | (m & act);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// finalize: posterior per codeword/bit, written row-major [b][N].
+//   BP : P = LR * prod lr (ascending row, dec.cpp:669-674), NaN -> 1
+//        (dec.cpp:676-677); iters == 0 -> P = LR (lr still 1 from init).
+//        post = log(P) (LDPC_POST_LLR) or P (LDPC_POST_RATIO).
+//   MSA: L = LLR + sum c2v (Decision_MSA_INF order); iters == 0 -> LLR.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ c2v, const double* __restrict__ prior,
+                                                  const int32_t* __restrict__ iters, const int32_t* __restrict__ col_ptr,
+                                                  const int32_t* __restrict__ col_edge, double* __restrict__ post,
+                                                  int algo_msa, int post_ratio, int64_t Bc, int32_t N, int64_t E)
+{
+    const int lane = lane_id();
+    const int32_t j = blockIdx.x * 4 + wave_id();
+    const int64_t t = blockIdx.y;
+    if (j >= N) return;
+    const int64_t b = t * TILE + lane;
+    if (b >= Bc) return;
+    const double pv = prior[((size_t)t * N + j) * TILE + lane];
+    const bool ran = iters[b] > 0;
+    const int32_t a = col_ptr[j], e1 = col_ptr[j + 1];
+    const size_t tb = (size_t)t * E;
+    double out;
+    if (algo_msa) {
+        double L = pv;
+        if (ran)
+            for (int32_t q = a; q < e1; ++q) L = L + c2v[(tb + col_edge[q]) * TILE + lane];
+        out = L;
+    } else {
+        double P = pv;
+        if (ran)
+            for (int32_t q = a; q < e1; ++q) P = P * c2v[(tb + col_edge[q]) * TILE + lane];
+        if (__builtin_isnan(P)) P = 1.0;
+        out = post_ratio ? P : log(P);
+    }
+    post[(size_t)b * N + j] = out;
+}
+
+// hard ballots -> [b][N] u8 (the reference's dblk / dec_*.txt bits)
+__global__ __launch_bounds__(256) void k_unpack_hard(const uint64_t* __restrict__ hard, uint8_t* __restrict__ out,
+                                                     int64_t Bc, int32_t N)
+{
+    const int64_t nj = (N + 255) / 256;
+    for (int64_t blk = blockIdx.x; blk < Bc * nj; blk += gridDim.x) {
+        const int64_t b = blk / nj;
+        const int32_t j = (int32_t)((blk - b * nj) * 256 + threadIdx.x);
+        if (j < N) out[(size_t)b * N + j] = (uint8_t)((hard[(size_t)(b >> 6) * N + j] >> (b & 63)) & 1ull);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic BSC channel, counter-based:
+//   u = splitmix64(((b << 24) | j) ^ splitmix64(seed)) >> 11, uniform in [0, 2^53)
+//   flip = u * 2^-53 < p;  y = codeword[b mod n_cw][j] ^ flip
+//   LLR = y ? -mag : +mag   (LR: y ? lr_neg : lr_pos, host-exp'd)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gen_bsc(double* __restrict__ out, int out_lr, int64_t b0, int64_t B,
+                                                 const uint8_t* __restrict__ cws, int32_t n_cw, int32_t N,
+                                                 uint64_t seedmix, double p, double pos, double negv)
+{
+    const int64_t total = B * (int64_t)N;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t bl = i / N;
+        const int32_t j = (int32_t)(i - bl * N);
+        const uint64_t b = (uint64_t)(b0 + bl);
+        const uint64_t u = splitmix64(((b << 24) | (uint64_t)j) ^ seedmix) >> 11;
+        const bool flip = (double)u * 0x1.0p-53 < p;
+        const uint8_t y = cws[(size_t)(b % (uint64_t)n_cw) * N + j] ^ (uint8_t)flip;
+        (void)out_lr;
+        out[i] = y ? negv : pos;
+    }
+}
+
+}  // namespace dev
+}  // namespace ldpc

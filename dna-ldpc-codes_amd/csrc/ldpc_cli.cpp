@@ -1,0 +1,244 @@
+// ldpc_cli.cpp -- file-compatible replacement of the reference's ldpc.exe for
+// the DNA pipeline's call (def_func.py:47-51):
+//
+//   ldpc <bSystematic> <decoder_type> <channel_type> <seed> <max_iter> <frame_num>
+//        [<target_frame_err> if frame_num == 0] <codeword_base> <soft_base> <pchk_base>
+//        <EbNo | eps (BEC) | p (BSC)> <punct> <short> <target> [<VN0> <VN1> if target]
+//
+// Argument parsing follows SetUp (DNA_main.cpp:300-505) for this subset;
+// decoder_type 0 = BP (dec.cpp:583), 20 = float min-sum (dec.cpp:1216, with
+// g_precision = 0, DNA_main.cpp:1293-1296, 1588-1594).  Inputs: <codeword>.txt
+// (N ints, error statistics only), <soft>.txt (N LLRs, LR = exp(LLR),
+// DNA_main.cpp:1319-1345), <pchk>.pchk.  Outputs: dec_<codeword>.txt ("%d "
+// per bit, DNA_main.cpp:916-927), result_(<soft>.txt)_<pchk>.pchk_... .txt
+// (Print_All_Result, DNA_main.cpp:965-1123), stdout summary (Set_Code :551-556,
+// Print_One_Result :1170-1182).  The decode itself runs on the GPU through the
+// C ABI; there is no CPU decode path.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <string>
+#include <vector>
+
+#include "../../include/ldpc_amd.h"
+
+static void die(const char* msg)
+{
+    std::fprintf(stderr, "%s\n", msg);
+    std::exit(1);
+}
+
+static bool read_tokens(const std::string& path, std::vector<std::string>& out, size_t need)
+{
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::string cur;
+    int ch;
+    while ((ch = std::fgetc(f)) != EOF && out.size() < need) {
+        if (ch == ' ' || ch == '\n' || ch == '\r' || ch == '\t') {
+            if (!cur.empty()) { out.push_back(cur); cur.clear(); }
+        } else {
+            cur.push_back((char)ch);
+        }
+    }
+    if (!cur.empty() && out.size() < need) out.push_back(cur);
+    std::fclose(f);
+    return true;
+}
+
+int main(int argc, char** argv)
+{
+    // ---- SetUp (DNA_main.cpp:300-331, 494-502) ----
+    int pos = 1;
+    auto arg = [&](void) -> const char* {
+        if (pos >= argc) { std::fprintf(stderr, "\n\nargc error!\n\n"); std::exit(1); }
+        return argv[pos++];
+    };
+    const int bSystematic = std::atoi(arg());
+    const int decoder_type = std::atoi(arg());
+    const int channel_type = std::atoi(arg());
+    const int seed = std::atoi(arg());
+    const int max_iter = std::atoi(arg());
+    const long frame_num = std::atol(arg());
+    int target_frame_err = 0;
+    if (frame_num == 0) target_frame_err = std::atoi(arg());
+    const std::string cw_base = arg();
+    const std::string soft_base = arg();
+    const std::string pchk_base = arg();
+    double EbNo = 0, eps = 0, p = 0;
+    if (channel_type == 2) eps = std::atof(arg());
+    else if (channel_type == 1) p = std::atof(arg());
+    else EbNo = std::atof(arg());
+    const int punct = std::atoi(arg());
+    const int shortening = std::atoi(arg());
+    const int targeting = std::atoi(arg());
+    int target_VN[2] = {0, 0};
+    if (targeting) { target_VN[0] = std::atoi(arg()); target_VN[1] = std::atoi(arg()); }
+    if (punct != 0 || shortening != 0) die("ldpc: puncturing/shortening are not supported by this build");
+    if (argc != pos) { std::fprintf(stderr, "\n\nargc error!\n\n"); return 1; }
+    int algo;
+    if (decoder_type == 0) algo = LDPC_ALGO_BP;
+    else if (decoder_type == 20) algo = LDPC_ALGO_MSA;
+    else die("ldpc: decoder_type must be 0 (BP) or 20 (min-sum)");
+    (void)eps; (void)p;
+
+    const std::string file_cw = cw_base + ".txt", file_soft = soft_base + ".txt", file_pchk = pchk_base + ".pchk";
+
+    // ---- Set_Code (DNA_main.cpp:544-609) ----
+    int err = 0;
+    ldpc_graph* g = ldpc_graph_load(file_pchk.c_str(), &err);
+    if (!g) { std::fprintf(stderr, "%s\n", ldpc_last_error()); return 1; }
+    int32_t M, N, dv, rdv, dc, rdc;
+    int64_t E;
+    ldpc_graph_info(g, &M, &N, &E, &dv, &rdv, &dc, &rdc);
+    const int K = N - M;
+    std::printf("\n");
+    std::printf("g_CODE_N : %d\n", N);
+    std::printf("g_CODE_K : %d\n", K);
+    std::printf("g_CODE_M : %d\n", M);
+    std::printf("\n");
+    if (!targeting) { target_VN[0] = 1; target_VN[1] = N; }
+    const double rate = 1.0 - (double)M / (double)N;
+    const double std_dev = 1 / std::sqrt(2 * rate * std::pow(10.0, EbNo * 0.1));  // getStd_dev channel.cpp:9-16
+
+    time_t t_start, t_end;
+    std::time(&t_start);
+
+    // ---- LDPC_Encode: read codeword + LLR (DNA_main.cpp:1319-1345) ----
+    std::vector<std::string> tok_cw, tok_soft;
+    if (!read_tokens(file_cw, tok_cw, (size_t)N)) { std::fprintf(stderr, "ldpc: cannot open %s\n", file_cw.c_str()); return 1; }
+    if (!read_tokens(file_soft, tok_soft, (size_t)N)) { std::fprintf(stderr, "ldpc: cannot open %s\n", file_soft.c_str()); return 1; }
+    if ((int)tok_cw.size() < N || (int)tok_soft.size() < N) die("ldpc: input file shorter than the code length");
+    std::vector<int> codeword((size_t)N);
+    std::vector<double> llr((size_t)N);
+    for (int i = 0; i < N; i++) {
+        codeword[(size_t)i] = std::atoi(tok_cw[(size_t)i].c_str());
+        llr[(size_t)i] = std::strtod(tok_soft[(size_t)i].c_str(), nullptr);  // fscanf %lf
+    }
+
+    // ---- LDPC_Channel raw error count (DNA_main.cpp:1711-1748) ----
+    const int len_raw = bSystematic ? K : N;
+    long long raw = 0;
+    for (int i = 0; i < len_raw; i++) {
+        int temp;
+        if (channel_type == 0) temp = llr[(size_t)i] >= 0 ? 0 : 1;
+        else if (channel_type == 2) { continue; }  // hard input never set -> no erasure marks
+        else temp = 0;                             // BSC: hard input never set (channel sims disabled)
+        if (codeword[(size_t)i] != temp) raw++;
+    }
+
+    // ---- LDPC_Decode on the GPU ----
+    std::vector<uint8_t> hard((size_t)N);
+    int32_t iters = 0;
+    uint8_t valid = 0;
+    ldpc_opts o{};
+    o.exp_on_host = 1;
+    if (ldpc_decode(g, llr.data(), 1, max_iter, algo, hard.data(), nullptr, &iters, &valid, &o) != LDPC_OK) {
+        std::fprintf(stderr, "ldpc: decode failed: %s\n", ldpc_last_error());
+        return 1;
+    }
+
+    // ---- LDPC_BIT_Check (DNA_main.cpp:1675-1706) ----
+    long long bit_err = 0;
+    if (bSystematic) {
+        for (int i = 0; i < K; i++) bit_err += codeword[(size_t)i] != hard[(size_t)i];
+    } else {
+        for (int i = target_VN[0] - 1; i < target_VN[1]; i++) bit_err += codeword[(size_t)i] != hard[(size_t)i];
+    }
+
+    // ---- frame loop bookkeeping (Check_End :756-795; Run_Simulation :800-912) ----
+    // Every frame re-reads the same files and decodes identically, so the
+    // counters scale with the number of frames.
+    long long frames;
+    if (frame_num == 0) {
+        if (target_frame_err <= 0) frames = 0;
+        else if (bit_err > 0) frames = target_frame_err;
+        else die("ldpc: frame_num 0 with an error-free decode never reaches the target frame-error count");
+    } else {
+        frames = frame_num;
+    }
+    long long frame_i[3] = {frames, frames, 0};
+    long long bit_errs[3] = {raw * frames, bit_err * frames, bit_err * frames};
+    long long frame_errs[3] = {raw > 0 ? frames : 0, bit_err > 0 ? frames : 0, bit_err > 0 ? frames : 0};
+
+    const std::string file_dec = "dec_" + cw_base + ".txt";
+    std::printf("%s", file_dec.c_str());
+    FILE* fd = std::fopen(file_dec.c_str(), "w");
+    if (!fd) die("ldpc: cannot write the decoded-word file");
+    for (int i = 0; i < N; i++) std::fprintf(fd, "%d ", frames > 0 ? (int)hard[(size_t)i] : 0);
+    std::fclose(fd);
+    std::time(&t_end);
+
+    // ---- Print_One_Result (DNA_main.cpp:1170-1182) ----
+    std::printf("\n");
+    if (channel_type == 2)
+        std::printf("[%d]  code : (%d,%d)\trate : %.3f\tEps : %.2f \n", 0, N, K, rate, eps);
+    else
+        std::printf("[%d]  code : (%d,%d)\trate : %.3f\tEb/No : %.2f dB\n", 0, N, K, rate, EbNo);
+    std::printf("[%d]  frame_num              : %lld\n", 0, frame_i[0]);
+    std::printf("[%d]  bit_err                : %lld\n", 0, bit_errs[2]);
+    std::printf("[%d]  frame_err              : %lld\n", 0, frame_errs[2]);
+    std::printf("[%d]  without coding (bit)   : %lld\n", 0, bit_errs[0]);
+    std::printf("[%d]  without coding (frame) : %lld\n\n", 0, frame_errs[0]);
+
+    // ---- Print_All_Result (DNA_main.cpp:965-1123) ----
+    const int len = bSystematic ? K : (target_VN[1] - target_VN[0] + 1);
+    const double denom = (double)len * (double)frame_i[0];
+    double BER[3];
+    for (int i = 0; i < 3; i++) BER[i] = (double)bit_errs[i] / denom;
+    const std::string file_soft_txt = soft_base + ".txt";
+    char name[4096];
+    if (channel_type == 2)
+        std::snprintf(name, sizeof name, "result_(%s)_%s_%d_%.3f_%d_%d_%d.txt", file_soft_txt.c_str(), file_pchk.c_str(),
+                      decoder_type, eps, 0, max_iter, seed);
+    else if (channel_type == 1)
+        std::snprintf(name, sizeof name, "result_(%s)_%s_%d_%.4f_%d_%d_%d.txt", file_soft_txt.c_str(), file_pchk.c_str(),
+                      decoder_type, p, 0, max_iter, seed);
+    else
+        std::snprintf(name, sizeof name, "result_(%s)_%s_%d_%.3fdB_%d_%d_%d.txt", file_soft_txt.c_str(),
+                      file_pchk.c_str(), decoder_type, EbNo, 0, max_iter, seed);
+    FILE* fr = std::fopen(name, "w");
+    if (!fr) die("ldpc: cannot write the result file");
+    std::fprintf(fr, "code N        : %d\n", N);
+    std::fprintf(fr, "code K        : %d\n", K);
+    std::fprintf(fr, "code M        : %d\n", M);
+    std::fprintf(fr, "code rate     : %.3f\n", rate);
+    if (channel_type == 2) {
+        std::fprintf(fr, "Eps\t\t: %.3f \n", eps);
+    } else {
+        std::fprintf(fr, "Eb/No         : %.2f dB\n", EbNo);
+        std::fprintf(fr, "g_std_dev     : %.2f\n", std_dev);
+    }
+    std::fprintf(fr, "max iteration : %d\n", max_iter);
+    std::fprintf(fr, "dv            : %d\n", dv);
+    std::fprintf(fr, "bRegular_dv   : %d\n", rdv);
+    std::fprintf(fr, "dc            : %d\n", dc);
+    std::fprintf(fr, "bRegular_dc   : %d\n", rdc);
+    if (targeting) std::fprintf(fr, "target_VN:%d~%d \n\n", target_VN[0], target_VN[1]);
+    std::fprintf(fr, "=============================================\n");
+    std::fprintf(fr, "                 result\n");
+    std::fprintf(fr, "=============================================\n");
+    double d = std::difftime(t_end, t_start);
+    const int hh = (int)(d / 3600);
+    d -= hh * 3600;
+    const int mm = (int)(d / 60);
+    d -= mm * 60;
+    const int ss = (int)d;
+    std::fprintf(fr, "start time      : %s", std::ctime(&t_start));
+    std::fprintf(fr, "end time        : %s", std::ctime(&t_end));
+    std::fprintf(fr, "simulation time : %d hours %d mins %d secs\n\n", hh, mm, ss);
+    std::fprintf(fr, "# of processes         : %d\n", 1);
+    std::fprintf(fr, "initial seed value     : %d\n\n", seed);
+    for (int i = 0; i < 2; i++) std::fprintf(fr, "# of Frame[%2d]          :%lld\n", i, frame_i[i]);
+    std::fprintf(fr, "\n");
+    for (int i = 0; i < 2; i++) std::fprintf(fr, "# of Bit Errors[%2d]     : %lld\n", i, bit_errs[i]);
+    std::fprintf(fr, "\n");
+    for (int i = 0; i < 2; i++) std::fprintf(fr, "BER[%2d]                 : %.5e\n", i, BER[i]);
+    std::fprintf(fr, "\n");
+    std::fclose(fr);
+    ldpc_graph_free(g);
+    (void)iters; (void)valid;
+    return 0;
+}

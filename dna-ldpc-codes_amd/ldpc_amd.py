@@ -1,0 +1,393 @@
+"""Python ctypes shim over lib/libldpc_amd.so (include/ldpc_amd.h).
+
+This is the in-process replacement for the reference pipeline's
+``write_bat(...); os.system('soft_decoder.bat'); file_read('dec_...')`` round
+trip (ex_decoder/decoder.py:553-562, 630-640; def_func.py:29-57): the .pchk is
+parsed once and cached, and a whole batch of LLR vectors is decoded per call on
+the GPU(s).
+
+    import ldpc_amd as L
+    hard, post, iters, valid = L.decode(llr, max_iter=200)          # llr: [B][N]
+    L.decode_files("codeword_n18432_m1860_1", "soft72000_n18432_m1860_1",
+                   "decode_n18432_m2048_final")                        # ldpc.exe side effects
+
+There is deliberately no CPU fallback: if the HIP library is missing or no GPU
+is visible, every decode raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+import threading
+import time
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libldpc_amd.so")
+
+LDPC_OK, LDPC_ERR_ARG, LDPC_ERR_IO, LDPC_ERR_FORMAT, LDPC_ERR_DEVICE, LDPC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
+ALGO_BP, ALGO_MSA = 0, 1
+POST_LLR, POST_RATIO = 0, 1
+IN_LLR, IN_LR = 0, 1
+H2D, D2H, D2D = 0, 1, 2
+
+# reference decoder_type values (DNA_main.cpp:41-53)
+_ALGOS = {"bp": ALGO_BP, 0: ALGO_BP, "msa": ALGO_MSA, "min-sum": ALGO_MSA, 20: ALGO_MSA}
+
+
+class LdpcError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ldpc_amd error {code}: {msg}")
+        self.code = code
+
+
+class Opts(C.Structure):
+    _fields_ = [("n_devices", C.c_int32), ("devices", C.POINTER(C.c_int32)), ("chunk", C.c_int64),
+                ("exp_on_host", C.c_int32), ("post_kind", C.c_int32), ("host_threads", C.c_int32),
+                ("reserved", C.c_int32 * 7)]
+
+
+class KernelStats(C.Structure):
+    _fields_ = [("launches", C.c_int64 * 6), ("ms", C.c_double * 6), ("edge_iters", C.c_int64),
+                ("cw_iters", C.c_int64)]
+
+
+KCLASS = ("check", "variable", "syndrome", "init", "finalize", "other")
+
+_lib = None
+_lib_lock = threading.Lock()
+
+EXPORTS = [
+    "ldpc_abi_version", "ldpc_last_error", "ldpc_device_count", "ldpc_graph_load", "ldpc_graph_from_edges",
+    "ldpc_graph_free", "ldpc_graph_info", "ldpc_graph_edges", "ldpc_graph_syndrome", "ldpc_decode",
+    "ldpc_engine_create", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
+    "ldpc_engine_gen_bsc", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
+    "ldpc_dev_memcpy",
+]
+
+
+def lib():
+    """Load the HIP library (fails loudly when it has not been built)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `make -C dna-ldpc-codes_amd` "
+                              "(there is no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        vp, i32, i64, dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+        pint = C.POINTER(C.c_int)
+        L.ldpc_abi_version.restype = C.c_int
+        L.ldpc_last_error.restype = C.c_char_p
+        L.ldpc_device_count.restype = C.c_int
+        L.ldpc_graph_load.argtypes = [C.c_char_p, pint]
+        L.ldpc_graph_load.restype = vp
+        L.ldpc_graph_from_edges.argtypes = [i32, i32, vp, vp, i64, pint]
+        L.ldpc_graph_from_edges.restype = vp
+        L.ldpc_graph_free.argtypes = [vp]
+        L.ldpc_graph_free.restype = None
+        L.ldpc_graph_info.argtypes = [vp] + [vp] * 7
+        L.ldpc_graph_edges.argtypes = [vp, vp, vp, vp, vp]
+        L.ldpc_graph_syndrome.argtypes = [vp, vp, vp]
+        L.ldpc_decode.argtypes = [vp, vp, i64, i32, i32, vp, vp, vp, vp, C.POINTER(Opts)]
+        L.ldpc_engine_create.argtypes = [vp, i32, i32, i64, pint]
+        L.ldpc_engine_create.restype = vp
+        L.ldpc_engine_free.argtypes = [vp]
+        L.ldpc_engine_free.restype = None
+        L.ldpc_engine_decode.argtypes = [vp, vp, i32, i64, i32, vp, vp, i32, vp, vp]
+        L.ldpc_engine_sync.argtypes = [vp]
+        L.ldpc_engine_stream.argtypes = [vp]
+        L.ldpc_engine_stream.restype = vp
+        L.ldpc_engine_gen_bsc.argtypes = [vp, vp, i32, i64, i64, vp, i32, C.c_uint64, dbl, dbl]
+        L.ldpc_engine_profile.argtypes = [vp, i32]
+        L.ldpc_engine_stats.argtypes = [vp, C.POINTER(KernelStats)]
+        L.ldpc_dev_malloc.argtypes = [i32, C.c_size_t]
+        L.ldpc_dev_malloc.restype = vp
+        L.ldpc_dev_free.argtypes = [i32, vp]
+        L.ldpc_dev_memcpy.argtypes = [i32, vp, vp, C.c_size_t, i32]
+        _lib = L
+        return L
+
+
+def _check(rc: int):
+    if rc != LDPC_OK:
+        raise LdpcError(rc, (lib().ldpc_last_error() or b"").decode(errors="replace"))
+    return rc
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def device_count() -> int:
+    return int(lib().ldpc_device_count())
+
+
+def _algo(a) -> int:
+    if isinstance(a, str):
+        a = a.lower()
+    if a not in _ALGOS:
+        raise ValueError(f"unknown algorithm {a!r} (use 'bp' or 'msa')")
+    return _ALGOS[a]
+
+
+class Graph:
+    """A parity-check graph loaded from a .pchk file (read_pchk, rcode.cpp:54-85)."""
+
+    def __init__(self, path: Optional[str] = None, *, handle=None):
+        if handle is None:
+            err = C.c_int(0)
+            handle = lib().ldpc_graph_load(os.fsencode(path), C.byref(err))
+            if not handle:
+                raise LdpcError(err.value, (lib().ldpc_last_error() or b"").decode(errors="replace"))
+        self._h = handle
+        self.path = path
+        M, N, dv, rdv, dc, rdc = (C.c_int32() for _ in range(6))
+        E = C.c_int64()
+        _check(lib().ldpc_graph_info(self._h, *[C.byref(x) for x in (M, N, E, dv, rdv, dc, rdc)]))
+        self.M, self.N, self.E = M.value, N.value, E.value
+        self.dv, self.regular_dv, self.dc, self.regular_dc = dv.value, bool(rdv.value), dc.value, bool(rdc.value)
+
+    @classmethod
+    def from_edges(cls, M: int, N: int, rows: Sequence[int], cols: Sequence[int]) -> "Graph":
+        r = np.ascontiguousarray(rows, dtype=np.int32)
+        c = np.ascontiguousarray(cols, dtype=np.int32)
+        err = C.c_int(0)
+        h = lib().ldpc_graph_from_edges(M, N, _ptr(r), _ptr(c), len(r), C.byref(err))
+        if not h:
+            raise LdpcError(err.value, (lib().ldpc_last_error() or b"").decode(errors="replace"))
+        return cls(handle=h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ldpc_graph_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def edges(self):
+        """(row_ptr[M+1], col_idx[E], col_ptr[N+1], col_edge[E]) int32 arrays."""
+        rp = np.zeros(self.M + 1, np.int32)
+        ci = np.zeros(max(self.E, 1), np.int32)
+        cp = np.zeros(self.N + 1, np.int32)
+        ce = np.zeros(max(self.E, 1), np.int32)
+        _check(lib().ldpc_graph_edges(self._h, _ptr(rp), _ptr(ci), _ptr(cp), _ptr(ce)))
+        return rp, ci[: self.E], cp, ce[: self.E]
+
+    def syndrome(self, dblk: np.ndarray):
+        """Number of unsatisfied checks and the parity vector (check.cpp:28-45)."""
+        d = np.ascontiguousarray(dblk, dtype=np.uint8)
+        if d.shape != (self.N,):
+            raise ValueError(f"dblk must have shape ({self.N},)")
+        pchk = np.zeros(self.M, np.uint8)
+        c = lib().ldpc_graph_syndrome(self._h, _ptr(d), _ptr(pchk))
+        if c < 0:
+            _check(c)
+        return int(c), pchk
+
+    def decode(self, llr: np.ndarray, max_iter: int = 200, algo="bp", post: Optional[str] = "llr",
+               devices: Optional[Sequence[int]] = None, chunk: int = 0, exp_on_host: bool = True,
+               host_threads: int = 0):
+        """Decode a batch of LLR vectors ([B][N] or [N]) on the GPU(s).
+
+        Returns (hard u8[B][N], post f64[B][N] or None, iters i32[B], valid bool[B]);
+        a 1-D input returns 1-D / scalar outputs.  post: 'llr' (log of the BP
+        posterior ratio / the min-sum L), 'ratio' (BP raw posterior ratio) or
+        None."""
+        a = _algo(algo)
+        x = np.ascontiguousarray(llr, dtype=np.float64)
+        single = x.ndim == 1
+        if single:
+            x = x[None, :]
+        if x.ndim != 2 or x.shape[1] != self.N:
+            raise ValueError(f"llr must have shape [B][{self.N}]")
+        B = x.shape[0]
+        hard = np.zeros((B, self.N), np.uint8)
+        postv = np.zeros((B, self.N), np.float64) if post else None
+        iters = np.zeros(B, np.int32)
+        valid = np.zeros(B, np.uint8)
+        o = Opts()
+        devs = None
+        if devices:
+            devs = (C.c_int32 * len(devices))(*devices)
+            o.n_devices = len(devices)
+            o.devices = C.cast(devs, C.POINTER(C.c_int32))
+        o.chunk = chunk
+        o.exp_on_host = 1 if exp_on_host else 0
+        o.post_kind = {None: POST_LLR, "llr": POST_LLR, "ratio": POST_RATIO}[post]
+        o.host_threads = host_threads
+        _check(lib().ldpc_decode(self._h, _ptr(x), B, int(max_iter), a, _ptr(hard), _ptr(postv), _ptr(iters),
+                                 _ptr(valid), C.byref(o)))
+        valid = valid.astype(bool)
+        if single:
+            return hard[0], (postv[0] if postv is not None else None), int(iters[0]), bool(valid[0])
+        return hard, postv, iters, valid
+
+
+# ---------------------------------------------------------------------------
+# module-level API: cached graphs (the .pchk is parsed once per process)
+# ---------------------------------------------------------------------------
+_graphs: dict = {}
+
+
+def graph(pchk_path: str) -> Graph:
+    key = os.path.abspath(pchk_path)
+    g = _graphs.get(key)
+    if g is None:
+        g = Graph(pchk_path)
+        _graphs[key] = g
+    return g
+
+
+def decode(llr: np.ndarray, max_iter: int = 200, algo="bp", pchk: Optional[str] = None, **kw):
+    """Batch decode with a cached graph (default: the DNA code shipped in tests/golden)."""
+    if pchk is None:
+        pchk = default_pchk()
+    return graph(pchk).decode(llr, max_iter=max_iter, algo=algo, **kw)
+
+
+def default_pchk() -> str:
+    return os.path.join(os.path.dirname(_HERE), "tests", "golden", "decode_n18432_m2048_final.pchk")
+
+
+# ---------------------------------------------------------------------------
+# ldpc.exe file contract, in-process (DNA_main.cpp:300-505, 916-927, 965-1123)
+# ---------------------------------------------------------------------------
+def _read_tokens(path: str, n: int, conv):
+    with open(path, "r") as f:
+        toks = f.read().split()
+    if len(toks) < n:
+        raise ValueError(f"{path}: expected {n} values, found {len(toks)}")
+    return [conv(t) for t in toks[:n]]
+
+
+def decode_files(codeword_base: str, soft_base: str, pchk_base: str, max_iter: int = 200, algo="bp",
+                 seed: int = 7, EbNo: float = 0.0, directory: str = ".") -> dict:
+    """Reproduce `ldpc 0 <algo> 0 <seed> <max_iter> 1 <codeword> <soft> <pchk> <EbNo> 0 0 0`
+    (def_func.write_bat) in-process: reads <codeword>.txt, <soft>.txt,
+    <pchk>.pchk from `directory`, writes dec_<codeword>.txt and the result file,
+    and returns the statistics.  decoder.py can replace its os.system call
+    (decoder.py:557-558, 635-636) with this."""
+    a = _algo(algo)
+    decoder_type = 0 if a == ALGO_BP else 20
+    j = lambda p: os.path.join(directory, p)  # noqa: E731
+    g = graph(j(pchk_base + ".pchk"))
+    N, M = g.N, g.M
+    K = N - M
+    t_start = time.time()
+    cw = np.array(_read_tokens(j(codeword_base + ".txt"), N, int), dtype=np.int64)
+    llr = np.array(_read_tokens(j(soft_base + ".txt"), N, float), dtype=np.float64)
+    raw = int(np.sum(cw != (llr < 0)))  # LDPC_Raw_Error_Check, AWGN soft decision (DNA_main.cpp:1727-1732)
+    hard, _, iters, valid = g.decode(llr, max_iter=max_iter, algo=a, post=None)
+    bit_err = int(np.sum(cw != hard))
+    with open(j("dec_" + codeword_base + ".txt"), "w") as f:
+        f.write("".join(f"{int(b)} " for b in hard))
+    t_end = time.time()
+    rate = 1.0 - M / N
+    std_dev = 1 / math.sqrt(2 * rate * math.pow(10.0, EbNo * 0.1))
+    name = "result_(%s.txt)_%s.pchk_%d_%.3fdB_%d_%d_%d.txt" % (soft_base, pchk_base, decoder_type, EbNo, 0,
+                                                             max_iter, seed)
+    d = int(t_end - t_start)
+    lines = [
+        f"code N        : {N}", f"code K        : {K}", f"code M        : {M}", "code rate     : %.3f" % rate,
+        "Eb/No         : %.2f dB" % EbNo, "g_std_dev     : %.2f" % std_dev, f"max iteration : {max_iter}",
+        f"dv            : {g.dv}", f"bRegular_dv   : {int(g.regular_dv)}", f"dc            : {g.dc}",
+        f"bRegular_dc   : {int(g.regular_dc)}", "=============================================",
+        "                 result", "=============================================",
+        "start time      : " + time.ctime(t_start), "end time        : " + time.ctime(t_end),
+        "simulation time : %d hours %d mins %d secs\n" % (d // 3600, (d % 3600) // 60, d % 60),
+        "# of processes         : 1", f"initial seed value     : {seed}\n",
+        "# of Frame[ 0]          :1", "# of Frame[ 1]          :1", "",
+        f"# of Bit Errors[ 0]     : {raw}", f"# of Bit Errors[ 1]     : {bit_err}", "",
+        "BER[ 0]                 : %.5e" % (raw / N), "BER[ 1]                 : %.5e" % (bit_err / N), "", "",
+    ]
+    with open(j(name), "w") as f:
+        f.write("\n".join(lines))
+    return {"iters": iters, "valid": valid, "bit_errors": bit_err, "raw_errors": raw, "hard": hard,
+            "dec_file": "dec_" + codeword_base + ".txt", "result_file": name}
+
+
+# ---------------------------------------------------------------------------
+# device-resident engine (bench / pipelines keeping data in HBM)
+# ---------------------------------------------------------------------------
+class DeviceBuffer:
+    def __init__(self, device: int, nbytes: int):
+        self.device, self.nbytes = device, nbytes
+        self.ptr = lib().ldpc_dev_malloc(device, nbytes)
+        if not self.ptr:
+            raise LdpcError(LDPC_ERR_DEVICE, (lib().ldpc_last_error() or b"").decode())
+
+    def upload(self, a: np.ndarray, offset: int = 0):
+        a = np.ascontiguousarray(a)
+        assert offset + a.nbytes <= self.nbytes
+        _check(lib().ldpc_dev_memcpy(self.device, C.c_void_p(self.ptr + offset), _ptr(a), a.nbytes, H2D))
+
+    def download(self, a: np.ndarray, offset: int = 0):
+        assert a.flags.c_contiguous and offset + a.nbytes <= self.nbytes
+        _check(lib().ldpc_dev_memcpy(self.device, _ptr(a), C.c_void_p(self.ptr + offset), a.nbytes, D2H))
+        return a
+
+    def at(self, offset: int):
+        return C.c_void_p(self.ptr + offset)
+
+    def free(self):
+        if self.ptr:
+            lib().ldpc_dev_free(self.device, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Engine:
+    def __init__(self, g: Graph, device: int = 0, algo="bp", chunk: int = 0):
+        self.g, self.device, self.algo = g, device, _algo(algo)
+        err = C.c_int(0)
+        self._h = lib().ldpc_engine_create(g.handle, device, self.algo, chunk, C.byref(err))
+        if not self._h:
+            raise LdpcError(err.value, (lib().ldpc_last_error() or b"").decode())
+
+    def decode(self, d_in, in_kind: int, B: int, max_iter: int, d_hard=None, d_post=None, post_kind=POST_LLR,
+               d_iters=None, d_valid=None):
+        _check(lib().ldpc_engine_decode(self._h, d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters,
+                                        d_valid))
+
+    def gen_bsc(self, d_out, out_kind: int, b0: int, B: int, d_cw, n_cw: int, seed: int, p: float, llr_mag: float):
+        _check(lib().ldpc_engine_gen_bsc(self._h, d_out, out_kind, b0, B, d_cw, n_cw, seed, p, llr_mag))
+
+    def sync(self):
+        _check(lib().ldpc_engine_sync(self._h))
+
+    def profile(self, enable: bool):
+        _check(lib().ldpc_engine_profile(self._h, 1 if enable else 0))
+
+    def stats(self) -> dict:
+        s = KernelStats()
+        _check(lib().ldpc_engine_stats(self._h, C.byref(s)))
+        return {k: {"launches": int(s.launches[i]), "ms": float(s.ms[i])} for i, k in enumerate(KCLASS)}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ldpc_engine_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

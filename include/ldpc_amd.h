@@ -1,0 +1,178 @@
+/*
+ * ldpc_amd.h -- C ABI of the MI355X-native batched LDPC decoder.
+ *
+ * Drop-in boundary for the `ldpc.exe` step of the DNA-storage pipeline of
+ * sjpark0905/DNA-LDPC-codes.  The reference crosses a process boundary once
+ * per codeword (ex_decoder/decoder.py:553-562 -> def_func.py:47-51 ->
+ * `ldpc 0 0 0 7 200 1 <codeword> <soft> <pchk> 0 0 0 0`), re-parses the .pchk
+ * each time and decodes one frame on one CPU thread.  This ABI replaces that
+ * with: load the .pchk once, decode a whole batch of LLR vectors per call on
+ * one or more GPUs.
+ *
+ * Plain C types only: pointers + sizes, caller-owned buffers.  The library
+ * owns device memory and the graph; a graph is immutable after load and may
+ * be shared by threads; every call is reentrant per handle (no globals beyond
+ * the thread-local error string).  Errors are negative return codes plus
+ * ldpc_last_error() -- never exit(), unlike the reference (rcode.cpp:61-79,
+ * mod2sparse.cpp:513-514).
+ *
+ * Arithmetic contract: IEEE fp64, reference operation order, bit-exact hard
+ * decisions / iteration counts with LDPC_dec/ldpc/dec.cpp.
+ */
+#ifndef LDPC_AMD_H
+#define LDPC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDPC_AMD_ABI_VERSION 1
+
+/* error codes */
+enum {
+    LDPC_OK = 0,
+    LDPC_ERR_ARG = -1,      /* bad argument */
+    LDPC_ERR_IO = -2,       /* cannot open / read a file */
+    LDPC_ERR_FORMAT = -3,   /* not a parity-check file / malformed */
+    LDPC_ERR_DEVICE = -4,   /* HIP runtime error, no device, out of memory */
+    LDPC_ERR_UNSUPPORTED = -5 /* graph shape outside the compiled kernels */
+};
+
+/* decoder algorithms (reference decoder_type, DNA_main.cpp:49, 1565-1594) */
+enum {
+    LDPC_ALGO_BP = 0,  /* sum-product, LR domain: Run_Belief_Propagation_Decoder dec.cpp:583 */
+    LDPC_ALGO_MSA = 1  /* float min-sum: Run_MSA_Decoder_INF dec.cpp:1216 (ldpc argv decoder_type 20) */
+};
+
+/* posterior output kinds (ldpc_opts.post_kind) */
+enum {
+    LDPC_POST_LLR = 0,   /* BP: log(P), P = LR*prod(lr) with NaN->1; MSA: L (already an LLR) */
+    LDPC_POST_RATIO = 1  /* BP only: the raw fp64 posterior likelihood ratio P (bit-exact checks) */
+};
+
+/* input kinds for device-resident decode */
+enum {
+    LDPC_IN_LLR = 0, /* ln(P0/P1); BP converts with exp() (on device: ocml exp) */
+    LDPC_IN_LR = 1   /* P0/P1 (BP only) -- what the reference feeds its BP (DNA_main.cpp:1344) */
+};
+
+typedef struct ldpc_graph ldpc_graph;
+
+typedef struct ldpc_opts {
+    int32_t n_devices;      /* <= 0: use device 0 only */
+    const int32_t *devices; /* device ordinals (NULL: 0..n_devices-1) */
+    int64_t chunk;          /* codewords resident per device per pass (0: auto) */
+    int32_t exp_on_host;    /* BP: compute LR = exp(LLR) with the host libm, exactly as
+                               DNA_main.cpp:1344 does (default 1 when opts == NULL) */
+    int32_t post_kind;      /* LDPC_POST_* */
+    int32_t host_threads;   /* threads for host exp/packing (0: auto) */
+    int32_t reserved[7];
+} ldpc_opts;
+
+/* ------------------------------------------------------------------------ */
+/* Graph                                                                     */
+/* ------------------------------------------------------------------------ */
+
+/* Load a Radford-Neal .pchk file.  Replaces read_pchk (rcode.cpp:54-85) +
+ * mod2sparse_read (mod2sparse.cpp:381-427): same magic ('P'<<8)+0x80, same
+ * record stream, same row/column ordering and duplicate rule
+ * (mod2sparse_insert, mod2sparse.cpp:502-604).  *err gets LDPC_OK or a code. */
+ldpc_graph *ldpc_graph_load(const char *pchk_path, int *err);
+
+/* Build a graph from (row, col) pairs (0-based).  Same ordering/dedup rules. */
+ldpc_graph *ldpc_graph_from_edges(int32_t M, int32_t N, const int32_t *rows, const int32_t *cols,
+                                  int64_t n_edges, int *err);
+
+void ldpc_graph_free(ldpc_graph *g);
+
+/* Dimensions and degrees (CheckRegular, dec.cpp:138-189). */
+int ldpc_graph_info(const ldpc_graph *g, int32_t *M, int32_t *N, int64_t *E, int32_t *dv_max,
+                    int32_t *regular_dv, int32_t *dc_max, int32_t *regular_dc);
+
+/* Copy out the CSR/CSC edge arrays (row_ptr[M+1], col_idx[E], col_ptr[N+1],
+ * col_edge[E]); any pointer may be NULL. */
+int ldpc_graph_edges(const ldpc_graph *g, int32_t *row_ptr, int32_t *col_idx, int32_t *col_ptr,
+                     int32_t *col_edge);
+
+/* Syndrome on the host: returns the number of unsatisfied checks for hard
+ * bits dblk[N] (check.cpp:28-45); pchk[M] (may be NULL) receives parities. */
+int ldpc_graph_syndrome(const ldpc_graph *g, const uint8_t *dblk, uint8_t *pchk);
+
+/* ------------------------------------------------------------------------ */
+/* Batched decode, host buffers (the in-process replacement of ldpc.exe)     */
+/* ------------------------------------------------------------------------ */
+
+/* Decode B codewords.  llr: [B][N] row-major fp64 channel LLRs ln(P0/P1) --
+ * what soft*.txt holds (decoder.py:314, 528-535).  Outputs (caller-owned,
+ * any of post/iters/valid may be NULL):
+ *   hard_out [B][N] u8  -- the reference's dblk / dec_*.txt bits
+ *   post_out [B][N] f64 -- per opts->post_kind
+ *   iters_out[B]    i32 -- return value of Run_*_Decoder (dec.cpp:604, 1249)
+ *   valid_out[B]    u8  -- *bIsCodeword (syndrome zero at exit)
+ * Replaces LDPC_Decode (DNA_main.cpp:1565-1594) for decoder_type 0 / 20. */
+int ldpc_decode(const ldpc_graph *g, const double *llr, int64_t B, int32_t max_iter, int32_t algo,
+                uint8_t *hard_out, double *post_out, int32_t *iters_out, uint8_t *valid_out,
+                const ldpc_opts *opts);
+
+/* ------------------------------------------------------------------------ */
+/* Device-resident engine (benchmarks, pipelines that keep data in HBM)      */
+/* ------------------------------------------------------------------------ */
+typedef struct ldpc_engine ldpc_engine;
+
+/* One engine = one device + one HIP stream + chunk-sized message buffers. */
+ldpc_engine *ldpc_engine_create(const ldpc_graph *g, int32_t device, int32_t algo, int64_t chunk, int *err);
+void ldpc_engine_free(ldpc_engine *e);
+
+/* Decode B codewords whose input already lives in device memory (d_in:
+ * [B][N] fp64, kind LDPC_IN_*).  Device outputs (NULL to skip): d_hard
+ * [B][N] u8, d_post [B][N] f64 (post_kind), d_iters [B] i32, d_valid [B] u8.
+ * Asynchronous on the engine's stream; ldpc_engine_sync() waits. */
+int ldpc_engine_decode(ldpc_engine *e, const double *d_in, int32_t in_kind, int64_t B, int32_t max_iter,
+                       uint8_t *d_hard, double *d_post, int32_t post_kind, int32_t *d_iters, uint8_t *d_valid);
+
+int ldpc_engine_sync(ldpc_engine *e);
+
+/* The engine's HIP stream (hipStream_t as void*). */
+void *ldpc_engine_stream(ldpc_engine *e);
+
+/* Synthetic BSC channel on device: for codeword
+ * index b in [b0, b0+B) and bit j, the transmitted bit is
+ * codewords[(b mod n_cw)][j] (d_codewords: [n_cw][N] u8 on device), flipped
+ * when hash(seed, b, j) < p; output value = +-llr_mag (LDPC_IN_LLR) or
+ * +-exp(+-llr_mag) with host-computed exp (LDPC_IN_LR), written to d_out
+ * [B][N] fp64. */
+int ldpc_engine_gen_bsc(ldpc_engine *e, double *d_out, int32_t out_kind, int64_t b0, int64_t B,
+                        const uint8_t *d_codewords, int32_t n_cw, uint64_t seed, double p, double llr_mag);
+
+/* Kernel timing (HIP events on the engine stream around every launch of
+ * each kernel class) -- enable before, read after ldpc_engine_sync(). */
+typedef struct ldpc_kernel_stats {
+    int64_t launches[6];    /* [0]=check [1]=variable [2]=syndrome [3]=init [4]=finalize [5]=other */
+    double ms[6];           /* summed device time per class */
+    int64_t edge_iters;     /* sum over launches of (live tiles * 64 * E) for check+variable */
+    int64_t cw_iters;       /* codeword-iterations executed (sum of iters) */
+} ldpc_kernel_stats;
+
+int ldpc_engine_profile(ldpc_engine *e, int32_t enable);
+int ldpc_engine_stats(ldpc_engine *e, ldpc_kernel_stats *out);
+
+/* Device buffers for callers without their own HIP allocator (bench, tests). */
+enum { LDPC_H2D = 0, LDPC_D2H = 1, LDPC_D2D = 2 };
+void *ldpc_dev_malloc(int32_t device, size_t bytes);
+int ldpc_dev_free(int32_t device, void *p);
+int ldpc_dev_memcpy(int32_t device, void *dst, const void *src, size_t bytes, int32_t kind);
+
+/* ------------------------------------------------------------------------ */
+/* misc                                                                      */
+/* ------------------------------------------------------------------------ */
+const char *ldpc_last_error(void); /* thread-local message for the last failing call */
+int ldpc_device_count(void);
+int ldpc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDPC_AMD_H */

@@ -1,0 +1,110 @@
+"""CPU tests of the C ABI: the library loads, exports exactly what
+include/ldpc_amd.h declares, and the host-side graph functions match the
+oracle.  No compute calls that need a GPU."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PCHK, ROOT
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "ldpc_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ldpc_[a-z_]+)\s*\(", src)))
+
+
+def test_exports_match_header(L):
+    declared = _declared()
+    assert len(declared) >= 20
+    out = subprocess.check_output(["nm", "-D", "--defined-only", L.LIB_PATH], text=True)
+    exported = sorted(set(m for m in re.findall(r" T (ldpc_\w+)", out)))
+    assert exported == declared
+    assert sorted(L.EXPORTS) == declared
+    lib = L.lib()
+    for name in declared:
+        assert hasattr(lib, name)
+    assert lib.ldpc_abi_version() == 1
+
+
+def test_graph_load_matches_oracle(L, og):
+    G = L.Graph(PCHK)
+    assert (G.M, G.N, G.E) == (og.M, og.N, og.E)
+    assert (G.dv, G.regular_dv, G.dc, G.regular_dc) == (8, True, 72, True)
+    rp, ci, cp, ce = G.edges()
+    assert np.array_equal(rp, og.row_ptr) and np.array_equal(ci, og.col_idx)
+    assert np.array_equal(cp, og.col_ptr) and np.array_equal(ce, og.col_edge)
+
+
+def test_host_syndrome_matches_oracle(L, og, codewords):
+    G = L.Graph(PCHK)
+    rng = np.random.default_rng(1)
+    for x in [codewords[0], codewords[271], (rng.random(G.N) < 0.3).astype(np.uint8)]:
+        c, p = G.syndrome(x)
+        c2, p2 = og.check(x)
+        assert c == c2 and np.array_equal(p, p2)
+
+
+def test_bad_files(L, tmp_path):
+    with pytest.raises(L.LdpcError) as e:
+        L.Graph(str(tmp_path / "missing.pchk"))
+    assert e.value.code == L.LDPC_ERR_IO
+    bad = tmp_path / "bad.pchk"
+    bad.write_bytes(b"\x00\x00\x00\x00" * 4)
+    with pytest.raises(L.LdpcError) as e:
+        L.Graph(str(bad))
+    assert e.value.code == L.LDPC_ERR_FORMAT
+    # truncated: no terminator (mod2sparse.cpp:421-426)
+    ints = np.array([(ord("P") << 8) + 0x80, 2, 3, -1, 1, 2], dtype="<i4")
+    trunc = tmp_path / "trunc.pchk"
+    ints.tofile(str(trunc))
+    with pytest.raises(L.LdpcError) as e:
+        L.Graph(str(trunc))
+    assert e.value.code == L.LDPC_ERR_FORMAT
+    # column before any row selector
+    ints = np.array([(ord("P") << 8) + 0x80, 2, 3, 1, 0], dtype="<i4")
+    p = tmp_path / "norow.pchk"
+    ints.tofile(str(p))
+    with pytest.raises(L.LdpcError):
+        L.Graph(str(p))
+    # column out of range
+    ints = np.array([(ord("P") << 8) + 0x80, 2, 3, -1, 4, 0], dtype="<i4")
+    ints.tofile(str(p))
+    with pytest.raises(L.LdpcError):
+        L.Graph(str(p))
+
+
+def test_ordering_and_dedup(L, oracle_mod, tmp_path):
+    # rows/cols given out of order with a duplicate -> sorted, deduplicated
+    ints = np.array([(ord("P") << 8) + 0x80, 3, 4, -2, 4, 1, 4, -1, 3, 2, -3, 1, 0], dtype="<i4")
+    p = tmp_path / "o.pchk"
+    ints.tofile(str(p))
+    G = L.Graph(str(p))
+    og = oracle_mod.OracleGraph(str(p))
+    rp, ci, cp, ce = G.edges()
+    assert G.E == 5
+    assert rp.tolist() == [0, 2, 4, 5] and ci.tolist() == [1, 2, 0, 3, 0]
+    assert np.array_equal(rp, og.row_ptr) and np.array_equal(ci, og.col_idx)
+    assert np.array_equal(cp, og.col_ptr) and np.array_equal(ce, og.col_edge)
+    G2 = L.Graph.from_edges(3, 4, [1, 1, 0, 0, 2, 1], [3, 0, 2, 1, 0, 3])
+    assert np.array_equal(G2.edges()[1], ci)
+
+
+def test_argument_validation_needs_no_gpu(L):
+    G = L.Graph(PCHK)
+    with pytest.raises(ValueError):
+        G.decode(np.zeros((2, 5)))
+    with pytest.raises(ValueError):
+        G.decode(np.zeros((1, G.N)), algo="gallager")
+    # B = 0 is a no-op that never touches a device
+    h, p, it, v = G.decode(np.zeros((0, G.N)))
+    assert h.shape == (0, G.N) and it.shape == (0,)
+
+
+def test_cli_rejects_bad_argc():
+    exe = os.path.join(ROOT, "dna-ldpc-codes_amd", "bin", "ldpc")
+    r = subprocess.run([exe, "0", "0", "0"], capture_output=True, text=True)
+    assert r.returncode == 1 and "argc error!" in r.stderr

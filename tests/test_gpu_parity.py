@@ -1,0 +1,209 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar (BASELINE.json north_star): hard decisions, iteration counts and valid
+flags bit-exact; BP posterior likelihood ratio bit-exact (fp64 bytes), the
+posterior LLR within 1e-5 (log differs only by device vs host libm).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import golden_cases
+import synth
+from conftest import GOLDEN, PCHK, pack
+
+pytestmark = pytest.mark.gpu
+POST_TOL = 1e-5
+
+
+def _cmp(G, og, llr, max_iter, algo="bp", **kw):
+    a = 0 if algo == "bp" else 1
+    ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, max_iter, algo=a, post_mode=1 if a == 0 else 0, threads=8)
+    post = "ratio" if a == 0 else "llr"
+    h, p, it, v = G.decode(llr, max_iter=max_iter, algo=algo, post=post, **kw)
+    assert np.array_equal(it, ref_it), (it, ref_it)
+    assert np.array_equal(v, ref_v.astype(bool))
+    assert np.array_equal(h, ref_h)
+    # posterior bit-exact (ratio for BP, L for min-sum) incl. inf; NaN never occurs here
+    assert np.array_equal(p.view(np.uint64), ref_p.view(np.uint64))
+    return h, p, it, v
+
+
+def test_dna_batch_272_bitexact_50_and_200(G, og, codewords):
+    """Config 2: the 272-codeword DNA batch, 50 and 200 iterations."""
+    llr = synth.dna_like_llrs(codewords, seed=0)
+    for it in (50, 200):
+        h, _, iters, v = _cmp(G, og, llr, it)
+        assert v.all() and np.array_equal(h, codewords)  # decoder.py:575-581 genie check
+
+
+def test_dna_near_threshold_bitexact(G, og, codewords):
+    llr = synth.dna_like_llrs(codewords, seed=1, reads=57000)[:96]
+    _, _, it, v = _cmp(G, og, llr, 200)
+    assert (it > 10).any() and not v.all()  # mixed early exits and a failure
+
+
+def test_posterior_llr_tolerance(G, og, codewords):
+    llr = synth.dna_like_llrs(codewords, seed=3, reads=60000)[:40]
+    _, ref_p, _, _ = og.decode_batch(llr, 50, post_mode=0, threads=8)
+    _, p, _, _ = G.decode(llr, max_iter=50, post="llr")
+    fin = np.isfinite(ref_p)
+    assert np.array_equal(fin, np.isfinite(p))
+    np.testing.assert_allclose(p[fin], ref_p[fin], rtol=0, atol=POST_TOL)
+
+
+def test_bsc_nonconverging_ragged(G, og, codewords):
+    """Config 3 shape at small B: p=0.02 never converges (exactly 50 iterations);
+    B = 70 -> one full tile + a ragged 6-codeword tile."""
+    llr = synth.bsc_llrs(codewords, 0, 70, seed=2026, p=0.02)
+    _, _, it, v = _cmp(G, og, llr, 50)
+    assert (it == 50).all() and not v.any()
+
+
+def test_bsc_converging(G, og, codewords):
+    llr = synth.bsc_llrs(codewords, 100, 64, seed=2026, p=0.004)
+    _, _, it, v = _cmp(G, og, llr, 50)
+    assert v.all()
+
+
+def test_min_sum_early_exit(G, og, codewords):
+    """Config 5 shape: min-sum with mixed early termination."""
+    llr = synth.bsc_llrs(codewords, 0, 130, seed=2026, p=0.002)
+    _, _, it, v = _cmp(G, og, llr, 50, algo="msa")
+    assert len(np.unique(it)) > 2
+
+
+def test_min_sum_nonconverging(G, og, codewords):
+    llr = synth.bsc_llrs(codewords, 0, 8, seed=7, p=0.01)
+    _cmp(G, og, llr, 20, algo="msa")
+
+
+def test_single_codeword_and_max_iter_zero(G, og, codewords):
+    llr = synth.bsc_llrs(codewords, 5, 1, seed=1, p=0.02)
+    _cmp(G, og, llr, 50)
+    _cmp(G, og, llr, 0)
+    _cmp(G, og, llr, 0, algo="msa")
+    h, p, it, v = G.decode(llr[0], max_iter=3)
+    assert h.shape == (18432,) and it == 3 and v is False
+
+
+def test_erasures_and_extreme_llrs(G, og, codewords):
+    """LLR 0 erasures (decoder.py:514-517), huge LLRs (LR overflow -> inf,
+    the NaN -> 1 guards of dec.cpp:676-677, 687-690) and -0.0."""
+    rng = np.random.default_rng(11)
+    llr = synth.bsc_llrs(codewords, 0, 64, seed=9, p=0.01)
+    llr[rng.random(llr.shape) < 0.05] = 0.0
+    llr[rng.random(llr.shape) < 0.01] *= 300.0  # exp(+-1167) -> inf / 0
+    llr[rng.random(llr.shape) < 0.01] = -0.0
+    _cmp(G, og, llr, 30)
+    _cmp(G, og, llr, 30, algo="msa")
+
+
+def test_multi_pass_chunking(G, og, codewords):
+    """B larger than the resident chunk: passes of 64 codewords."""
+    llr = synth.bsc_llrs(codewords, 0, 150, seed=4, p=0.006)
+    _cmp(G, og, llr, 25, chunk=64)
+
+
+def test_golden_vectors(G):
+    z = np.load(f"{GOLDEN}/oracle_goldens.npz", allow_pickle=False)
+    for case in golden_cases.CASES:
+        llr, max_iter, algo = golden_cases.inputs(case, z)
+        h, p, it, v = G.decode(llr, max_iter=max_iter, algo="bp" if algo == 0 else "msa",
+                               post="ratio" if algo == 0 else "llr")
+        assert np.array_equal(pack(h), z[case + "_hard"]), case
+        assert np.array_equal(it, z[case + "_iters"]), case
+        assert np.array_equal(v, z[case + "_valid"].astype(bool)), case
+        assert hashlib.sha256(p.tobytes()).hexdigest() == str(z[case + "_post_sha"]), case
+
+
+def test_irregular_graph_generic_kernels(gpu, oracle_mod, tmp_path):
+    """Irregular degrees exercise the generic (non-template) kernels, incl.
+    a degree-1 row, an empty row and an empty column."""
+    rng = np.random.default_rng(3)
+    M, N = 40, 120
+    rows, cols = [], []
+    for j in range(N - 1):  # column N-1 stays empty
+        for i in rng.choice(M - 1, size=int(rng.integers(1, 5)), replace=False):  # row M-1 stays empty
+            rows.append(int(i)); cols.append(j)
+    rows.append(5); cols.append(7)  # duplicate entry: ignored (mod2sparse.cpp:521-524)
+    # write a .pchk so both sides load the same file
+    path = tmp_path / "irr.pchk"
+    _write_pchk(path, M, N, rows, cols)
+    og = oracle_mod.OracleGraph(str(path))
+    G = gpu.Graph(str(path))
+    assert (G.M, G.N, G.E) == (og.M, og.N, og.E)
+    llr = rng.normal(2.0, 2.5, size=(70, N))
+    llr[:, :5] = 0.0
+    _cmp(G, og, llr, 40)
+    _cmp(G, og, llr, 40, algo="msa")
+
+
+def _write_pchk(path, M, N, rows, cols):
+    by_row = {}
+    for r, c in zip(rows, cols):
+        by_row.setdefault(r, []).append(c)
+    ints = [(ord("P") << 8) + 0x80, M, N]
+    for r in sorted(by_row):
+        ints.append(-(r + 1))
+        ints.extend(c + 1 for c in by_row[r])
+    ints.append(0)
+    np.array(ints, dtype="<i4").tofile(str(path))
+
+
+def test_device_bsc_generator_matches_host(gpu, G, codewords):
+    L = gpu
+    eng = L.Engine(G, 0, "bp", chunk=64)
+    B, N = 100, G.N
+    cwbuf = L.DeviceBuffer(0, codewords.nbytes)
+    cwbuf.upload(codewords)
+    out = L.DeviceBuffer(0, B * N * 8)
+    for kind, as_lr in ((L.IN_LLR, False), (L.IN_LR, True)):
+        eng.gen_bsc(out.at(0), kind, 12345, B, cwbuf.at(0), 272, 2026, 0.02, synth.LLR_UNIT)
+        eng.sync()
+        got = out.download(np.empty((B, N), np.float64))
+        exp = synth.bsc_llrs(codewords, 12345, B, seed=2026, p=0.02, as_lr=as_lr)
+        assert np.array_equal(got, exp)
+
+
+def test_engine_device_resident_matches_host_api(gpu, G, og, codewords):
+    """ldpc_engine_decode on device-resident LR input == ldpc_decode == oracle,
+    including hard/iters/valid outputs and profiling counters."""
+    L = gpu
+    B, N = 130, G.N
+    eng = L.Engine(G, 0, "bp", chunk=128)  # 2 passes
+    cwbuf = L.DeviceBuffer(0, codewords.nbytes)
+    cwbuf.upload(codewords)
+    din = L.DeviceBuffer(0, B * N * 8)
+    eng.gen_bsc(din.at(0), L.IN_LR, 0, B, cwbuf.at(0), 272, 77, 0.005, synth.LLR_UNIT)
+    dh, dit, dv = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
+    eng.profile(True)
+    eng.decode(din.at(0), L.IN_LR, B, 50, dh.at(0), None, L.POST_LLR, dit.at(0), dv.at(0))
+    eng.sync()
+    st = eng.stats()
+    assert st["check"]["launches"] > 0 and st["check"]["ms"] > 0
+    h = dh.download(np.empty((B, N), np.uint8))
+    it = dit.download(np.empty(B, np.int32))
+    v = dv.download(np.empty(B, np.uint8))
+    llr = synth.bsc_llrs(codewords, 0, B, seed=77, p=0.005)
+    rh, _, rit, rv = og.decode_batch(llr, 50, threads=8, want_post=False)
+    assert np.array_equal(it, rit) and np.array_equal(v, rv) and np.array_equal(h, rh)
+
+
+def test_device_exp_matches_host_on_dna_alphabet(gpu, G, codewords):
+    """LLR input with exp on the device (ocml) vs the host libm: on the DNA
+    alphabet k*ln49 the decode is identical (the survey's exhaustive exp check)."""
+    llr = synth.dna_like_llrs(codewords, seed=0, reads=60000)[:64]
+    a = G.decode(llr, max_iter=50, post="ratio", exp_on_host=True)
+    b = G.decode(llr, max_iter=50, post="ratio", exp_on_host=False)
+    ks = np.unique(np.rint(llr / synth.LLR_UNIT))
+    assert len(ks) > 5
+    for x, y in zip(a, b):
+        assert np.array_equal(np.asarray(x), np.asarray(y))
+
+
+def test_multi_device_api_single_gpu_box(G, og, codewords):
+    """devices=[0,0]: two host threads sharing one GPU exercise the sharded path."""
+    llr = synth.bsc_llrs(codewords, 0, 100, seed=8, p=0.006)
+    _cmp(G, og, llr, 20, devices=[0, 0])
