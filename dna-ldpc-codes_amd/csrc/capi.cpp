@@ -283,15 +283,31 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
     return LDPC_OK;
 }
 
-ldpc_engine* ldpc_engine_create(const ldpc_graph* g, int32_t device, int32_t algo, int64_t chunk, int* err)
+ldpc_engine* ldpc_engine_create_ex(const ldpc_graph* g, int32_t device, int32_t algo, int64_t chunk,
+                                   int64_t group_tiles, int32_t flags, int* err)
 {
     if (!g) { set_error("null graph"); fail(LDPC_ERR_ARG, err); return nullptr; }
     auto e = std::make_unique<ldpc_engine>();
     e->e = std::make_unique<Engine>();
-    int rc = e->e->init(&g->h, device, algo, chunk);
+    int rc = e->e->init(&g->h, device, algo, chunk, group_tiles, flags < 0 ? -1 : (flags & 1),
+                        flags < 0 ? -1 : ((flags >> 1) & 1), flags < 0 ? -1 : ((flags >> 2) & 1));
     if (rc) { fail(rc, err); return nullptr; }
     if (err) *err = LDPC_OK;
     return e.release();
+}
+
+ldpc_engine* ldpc_engine_create(const ldpc_graph* g, int32_t device, int32_t algo, int64_t chunk, int* err)
+{
+    return ldpc_engine_create_ex(g, device, algo, chunk, -1, -1, err);
+}
+
+int ldpc_engine_info(ldpc_engine* e, int64_t* cap, int64_t* group_tiles, int32_t* flags)
+{
+    if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
+    if (cap) *cap = e->e->cap;
+    if (group_tiles) *group_tiles = e->e->group_tiles;
+    if (flags) *flags = (e->e->nt_d ? 1 : 0) | (e->e->pipe ? 2 : 0) | (e->e->lr_csc ? 4 : 0);
+    return LDPC_OK;
 }
 
 void ldpc_engine_free(ldpc_engine* e) { delete e; }
@@ -321,13 +337,13 @@ int ldpc_engine_gen_bsc(ldpc_engine* e, double* d_out, int32_t out_kind, int64_t
     return e->e->gen_bsc(d_out, out_kind, b0, B, d_codewords, n_cw, seed, p, llr_mag);
 }
 
-int ldpc_engine_profile(ldpc_engine* e, int32_t enable)
+int ldpc_engine_profile(ldpc_engine* e, int32_t stride)
 {
     if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
     int rc = e->e->collect_stats();
     if (rc) return rc;
-    for (int c = 0; c < ldpc::K_NCLASS; c++) { e->e->launches[c] = 0; e->e->ms[c] = 0; }
-    e->e->profile = enable != 0;
+    for (int c = 0; c < ldpc::K_NCLASS; c++) { e->e->launches[c] = 0; e->e->ms[c] = 0; e->e->sampled[c] = 0; }
+    e->e->profile_stride = stride > 0 ? stride : 0;
     return LDPC_OK;
 }
 
@@ -337,7 +353,11 @@ int ldpc_engine_stats(ldpc_engine* e, ldpc_kernel_stats* out)
     int rc = e->e->collect_stats();
     if (rc) return rc;
     std::memset(out, 0, sizeof(*out));
-    for (int c = 0; c < ldpc::K_NCLASS; c++) { out->launches[c] = e->e->launches[c]; out->ms[c] = e->e->ms[c]; }
+    for (int c = 0; c < ldpc::K_NCLASS; c++) {
+        out->launches[c] = e->e->launches[c];
+        out->sampled[c] = e->e->sampled[c];
+        out->ms[c] = e->e->ms[c];
+    }
     return LDPC_OK;
 }
 

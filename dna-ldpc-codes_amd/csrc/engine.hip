@@ -26,7 +26,14 @@
 #include "engine.hpp"
 #include "kernels.hpp"
 
+#include <cstdlib>
+
 namespace ldpc {
+
+constexpr int64_t kDefaultGroupTiles = 3;  // tools/sweep.py on MI355X
+constexpr int64_t kDefaultNT = 1;
+constexpr int64_t kDefaultPipe = 0;
+constexpr int64_t kDefaultCsc = 0;
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
@@ -42,12 +49,21 @@ Engine::~Engine()
 {
     if (device >= 0) hipSetDevice(device);
     if (stream) hipStreamSynchronize(stream);
+    if (stream2) hipStreamSynchronize(stream2);
+    for (int i = 0; i < 2; i++) {
+        if (ev_chk[i]) hipEventDestroy(ev_chk[i]);
+        if (ev_var[i]) hipEventDestroy(ev_var[i]);
+    }
+    if (ev_join) hipEventDestroy(ev_join);
     for (int c = 0; c < K_NCLASS; c++)
         for (auto& p : ev_live[c]) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
     for (auto e : ev_pool) hipEventDestroy(e);
+    hipFree(d_csc_pos);
     hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge);
     hipFree(v2c); hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
+    hipFree(post_t);
     if (stream) hipStreamDestroy(stream);
+    if (stream2) hipStreamDestroy(stream2);
 }
 
 template <typename T>
@@ -59,7 +75,14 @@ static int upload(T** dst, const std::vector<T>& v)
     return LDPC_OK;
 }
 
-int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk)
+static int64_t env_int(const char* name, int64_t dflt)
+{
+    const char* v = std::getenv(name);
+    return (v && *v) ? std::atoll(v) : dflt;
+}
+
+int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, int64_t group, int nt, int pipelined,
+                 int csc)
 {
     g = graph;
     device = dev;
@@ -80,6 +103,23 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk)
     cap = std::max<int64_t>(64, (chunk + 63) / 64 * 64);
     cap_tiles = cap / 64;
     if (cap_tiles > 65535) { set_error("chunk too large (max 4194240 codewords)"); return LDPC_ERR_ARG; }
+    // group: tiles whose check->variable messages are live at once.  Small
+    // groups keep c2v resident in the 256 MB Infinity Cache between the check
+    // and the variable phase; 0 = the whole pass.
+    if (group < 0) group = env_int("LDPC_GROUP_TILES", kDefaultGroupTiles);
+    if (nt < 0) nt = (int)env_int("LDPC_NT_D", kDefaultNT);
+    group_tiles = (group <= 0 || group > cap_tiles) ? cap_tiles : group;
+    nt_d = nt != 0;
+    if (pipelined < 0) pipelined = (int)env_int("LDPC_PIPE", kDefaultPipe);
+    pipe = pipelined != 0 && group_tiles < cap_tiles;
+    if (pipe) {
+        LDPC_HIP(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+        for (int i = 0; i < 2; i++) {
+            LDPC_HIP(hipEventCreateWithFlags(&ev_chk[i], hipEventDisableTiming));
+            LDPC_HIP(hipEventCreateWithFlags(&ev_var[i], hipEventDisableTiming));
+        }
+        LDPC_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    }
 
     int rc;
     if ((rc = upload(&d_row_ptr, g->row_ptr)) || (rc = upload(&d_col_idx, g->col_idx)) ||
@@ -91,9 +131,16 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk)
             for (int k = 0; k < g->dc_max; k++) T[(size_t)k * g->M + i] = g->col_idx[(size_t)i * g->dc_max + k];
         if ((rc = upload(&d_col_idx_T, T))) return rc;
     }
+    {
+        std::vector<int32_t> pos((size_t)std::max<int64_t>(g->E, 1), 0);
+        for (size_t q = 0; q < g->col_edge.size(); q++) pos[(size_t)g->col_edge[q]] = (int32_t)q;
+        if ((rc = upload(&d_csc_pos, pos))) return rc;
+    }
+    if (csc < 0) csc = (int)env_int("LDPC_LR_CSC", kDefaultCsc);
+    lr_csc = csc != 0 && g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
     const size_t E = (size_t)std::max<int64_t>(g->E, 1);
     LDPC_HIP(hipMalloc((void**)&v2c, (size_t)cap * E * sizeof(double)));
-    LDPC_HIP(hipMalloc((void**)&c2v, (size_t)cap * E * sizeof(double)));
+    LDPC_HIP(hipMalloc((void**)&c2v, (size_t)(pipe ? 2 : 1) * group_tiles * 64 * E * sizeof(double)));
     LDPC_HIP(hipMalloc((void**)&prior, (size_t)cap * g->N * sizeof(double)));
     LDPC_HIP(hipMalloc((void**)&hard, (size_t)cap_tiles * g->N * sizeof(uint64_t)));
     LDPC_HIP(hipMalloc((void**)&active, (size_t)cap_tiles * sizeof(uint64_t)));
@@ -110,24 +157,25 @@ hipEvent_t Engine::get_event()
     return e;
 }
 
-int Engine::mark_begin(KClass c, hipEvent_t* b)
+int Engine::mark_begin(KClass c, hipStream_t s, hipEvent_t* b)
 {
-    launches[c]++;
+    const int64_t idx = launches[c]++;
     *b = nullptr;
-    if (!profile) return LDPC_OK;
+    if (profile_stride <= 0 || idx % profile_stride != 0) return LDPC_OK;
+    sampled[c]++;
     *b = get_event();
     if (!*b) { set_error("hipEventCreate failed"); return LDPC_ERR_DEVICE; }
-    LDPC_HIP(hipEventRecord(*b, stream));
+    LDPC_HIP(hipEventRecord(*b, s));
     return LDPC_OK;
 }
 
-int Engine::mark_end(KClass c, hipEvent_t b)
+int Engine::mark_end(KClass c, hipStream_t s, hipEvent_t b)
 {
     LDPC_HIP(hipGetLastError());
-    if (!profile || !b) return LDPC_OK;
+    if (!b) return LDPC_OK;
     hipEvent_t e = get_event();
     if (!e) { set_error("hipEventCreate failed"); return LDPC_ERR_DEVICE; }
-    LDPC_HIP(hipEventRecord(e, stream));
+    LDPC_HIP(hipEventRecord(e, s));
     ev_live[c].push_back({b, e});
     return LDPC_OK;
 }
@@ -136,6 +184,7 @@ int Engine::collect_stats()
 {
     LDPC_HIP(hipSetDevice(device));
     LDPC_HIP(hipStreamSynchronize(stream));
+    if (stream2) LDPC_HIP(hipStreamSynchronize(stream2));
     for (int c = 0; c < K_NCLASS; c++) {
         for (auto& p : ev_live[c]) {
             float t = 0.f;
@@ -149,15 +198,88 @@ int Engine::collect_stats()
     return LDPC_OK;
 }
 
-#define LAUNCH(cls, ...)                                  \
+#define LAUNCH_ON(strm, cls, ...)                         \
     do {                                                  \
         hipEvent_t _b;                                    \
-        int _rc = mark_begin(cls, &_b);                   \
+        int _rc = mark_begin(cls, strm, &_b);             \
         if (_rc) return _rc;                              \
         __VA_ARGS__;                                      \
-        _rc = mark_end(cls, _b);                          \
+        _rc = mark_end(cls, strm, _b);                    \
         if (_rc) return _rc;                              \
     } while (0)
+#define LAUNCH(cls, ...) LAUNCH_ON(stream, cls, __VA_ARGS__)
+
+// check phase of tiles t0 .. t0+gt-1 into `scratch` (that group's c2v)
+template <bool NT, bool CSCL>
+static void check_regular(int algo, hipStream_t s, dim3 grid, const double* v2c, double* scratch, const uint64_t* active,
+                          const int32_t* pos, int32_t M, int64_t E, int64_t t0)
+{
+    using namespace dev;
+    if (algo == LDPC_ALGO_BP)
+        hipLaunchKernelGGL((k_check_bp<72, NT, CSCL>), grid, dim3(256), 0, s, v2c, scratch, active, pos, M, E, t0);
+    else
+        hipLaunchKernelGGL((k_check_msa<72, NT, CSCL>), grid, dim3(256), 0, s, v2c, scratch, active, pos, M, E, t0);
+}
+
+template <bool NT, bool CSCL>
+static void var_regular(int algo, hipStream_t s, dim3 grid, const double* scratch, double* v2c, const double* prior,
+                        uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N,
+                        int64_t E, int64_t t0)
+{
+    using namespace dev;
+    if (algo == LDPC_ALGO_BP)
+        hipLaunchKernelGGL((k_var_bp<8, NT, CSCL>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active, col_edge,
+                           pt, N, E, t0);
+    else
+        hipLaunchKernelGGL((k_var_msa<8, NT, CSCL>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active, col_edge,
+                           pt, N, E, t0);
+}
+
+int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt)
+{
+    using namespace dev;
+    const int32_t M = g->M;
+    const int64_t E = g->E;
+    const bool reg72 = g->regular_dc && g->dc_max == 72;
+    const dim3 grid((M + 3) / 4, gt), blk(256);
+    if (reg72) {
+        LAUNCH_ON(s, K_CHECK, {
+            if (nt_d && lr_csc) check_regular<true, true>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0);
+            else if (nt_d) check_regular<true, false>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0);
+            else if (lr_csc) check_regular<false, true>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0);
+            else check_regular<false, false>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0);
+        });
+    } else if (algo == LDPC_ALGO_BP) {
+        LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL(k_check_bp_gen, grid, blk, 0, s, v2c, scratch, active, d_row_ptr, M, E, t0));
+    } else {
+        LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL(k_check_msa_gen, grid, blk, 0, s, v2c, scratch, active, d_row_ptr, M, E, t0));
+    }
+    return LDPC_OK;
+}
+
+// variable phase (+ hard decisions, optional posterior) of tiles t0 .. t0+gt-1
+int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt)
+{
+    using namespace dev;
+    const int32_t N = g->N;
+    const int64_t E = g->E;
+    const bool reg8 = g->regular_dv && g->dv_max == 8;
+    const dim3 grid((N + 3) / 4, gt), blk(256);
+    if (reg8) {
+        // lr_csc implies both phases use the regular kernels
+        LAUNCH_ON(s, K_VAR, {
+            if (nt_d && lr_csc) var_regular<true, true>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0);
+            else if (nt_d) var_regular<true, false>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0);
+            else if (lr_csc) var_regular<false, true>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0);
+            else var_regular<false, false>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0);
+        });
+    } else if (algo == LDPC_ALGO_BP) {
+        LAUNCH_ON(s, K_VAR, hipLaunchKernelGGL(k_var_bp_gen, grid, blk, 0, s, scratch, v2c, prior, hard, active, d_col_ptr, d_col_edge, pt, N, E, t0));
+    } else {
+        LAUNCH_ON(s, K_VAR, hipLaunchKernelGGL(k_var_msa_gen, grid, blk, 0, s, scratch, v2c, prior, hard, active, d_col_ptr, d_col_edge, pt, N, E, t0));
+    }
+    return LDPC_OK;
+}
 
 int Engine::run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_iter, uint8_t* d_hard,
                       double* d_post, int post_kind, int32_t* d_iters, uint8_t* d_valid)
@@ -169,14 +291,13 @@ int Engine::run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_i
     const int msa = algo == LDPC_ALGO_MSA;
     if (msa && in_kind == LDPC_IN_LR) { set_error("min-sum takes LLR input"); return LDPC_ERR_ARG; }
     if (msa && post_kind == LDPC_POST_RATIO) { set_error("LDPC_POST_RATIO is BP-only"); return LDPC_ERR_ARG; }
-    const bool reg_row72 = g->regular_dc && g->dc_max == 72;
-    const bool reg_col8 = g->regular_dv && g->dv_max == 8;
     const bool reg_rowT = g->regular_dc && d_col_idx_T != nullptr;
+    if (d_post && !post_t) LDPC_HIP(hipMalloc((void**)&post_t, (size_t)cap * N * sizeof(double)));
+    double* pt = d_post ? post_t : nullptr;
 
     const dim3 blk(256);
     const dim3 g_init((N + 63) / 64, (unsigned)tiles);
-    const dim3 g_rows((M + 3) / 4, (unsigned)tiles);
-    const dim3 g_cols((N + 3) / 4, (unsigned)tiles);
+    const dim3 g_cols_all((N + 3) / 4, (unsigned)tiles);
 
     LAUNCH(K_INIT, hipLaunchKernelGGL(k_init, g_init, blk, 0, stream, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, msa, Bc, N,
                                       E, d_col_ptr, d_col_edge, prior, v2c, hard, active, iters, valid));
@@ -188,35 +309,36 @@ int Engine::run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_i
             LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome<0>, dim3((unsigned)tiles), dim3(1024), 0, stream, hard, active,
                                              iters, valid, d_row_ptr, d_col_idx, d_col_idx_T, M, N, n, max_iter));
         if (n >= max_iter) break;
-        if (!msa) {
-            if (reg_row72)
-                LAUNCH(K_CHECK, hipLaunchKernelGGL(k_check_bp<72>, g_rows, blk, 0, stream, v2c, c2v, active, M, E));
-            else
-                LAUNCH(K_CHECK, hipLaunchKernelGGL(k_check_bp_gen, g_rows, blk, 0, stream, v2c, c2v, active, d_row_ptr,
-                                                   M, E));
-            if (reg_col8)
-                LAUNCH(K_VAR, hipLaunchKernelGGL(k_var_bp<8>, g_cols, blk, 0, stream, c2v, v2c, prior, hard, active,
-                                                 d_col_edge, N, E));
-            else
-                LAUNCH(K_VAR, hipLaunchKernelGGL(k_var_bp_gen, g_cols, blk, 0, stream, c2v, v2c, prior, hard, active,
-                                                 d_col_ptr, d_col_edge, N, E));
-        } else {
-            if (reg_row72)
-                LAUNCH(K_CHECK, hipLaunchKernelGGL(k_check_msa<72>, g_rows, blk, 0, stream, v2c, c2v, active, M, E));
-            else
-                LAUNCH(K_CHECK, hipLaunchKernelGGL(k_check_msa_gen, g_rows, blk, 0, stream, v2c, c2v, active,
-                                                   d_row_ptr, M, E));
-            if (reg_col8)
-                LAUNCH(K_VAR, hipLaunchKernelGGL(k_var_msa<8>, g_cols, blk, 0, stream, c2v, v2c, prior, hard, active,
-                                                 d_col_edge, N, E));
-            else
-                LAUNCH(K_VAR, hipLaunchKernelGGL(k_var_msa_gen, g_cols, blk, 0, stream, c2v, v2c, prior, hard, active,
-                                                 d_col_ptr, d_col_edge, N, E));
+        // groups of G tiles: check(group) then variable(group); with `pipe`,
+        // check(g+1) on `stream` overlaps variable(g) on `stream2` and the
+        // c2v scratch is double-buffered (slot g & 1).
+        const size_t slot_elems = (size_t)group_tiles * 64 * (size_t)E;
+        int64_t gi = 0;
+        for (int64_t t0 = 0; t0 < tiles; t0 += group_tiles, gi++) {
+            const unsigned gt = (unsigned)std::min<int64_t>(group_tiles, tiles - t0);
+            const int slot = pipe ? (int)(gi & 1) : 0;
+            double* scratch = c2v + (size_t)slot * slot_elems;
+            int rc;
+            if (!pipe) {
+                if ((rc = launch_check(stream, scratch, t0, gt))) return rc;
+                if ((rc = launch_var(stream, scratch, t0, gt, pt))) return rc;
+                continue;
+            }
+            if (gi >= 2) LDPC_HIP(hipStreamWaitEvent(stream, ev_var[slot], 0));  // slot free again
+            if ((rc = launch_check(stream, scratch, t0, gt))) return rc;
+            LDPC_HIP(hipEventRecord(ev_chk[slot], stream));
+            LDPC_HIP(hipStreamWaitEvent(stream2, ev_chk[slot], 0));
+            if ((rc = launch_var(stream2, scratch, t0, gt, pt))) return rc;
+            LDPC_HIP(hipEventRecord(ev_var[slot], stream2));
+        }
+        if (pipe) {  // the next syndrome needs every variable phase of this iteration
+            LDPC_HIP(hipEventRecord(ev_join, stream2));
+            LDPC_HIP(hipStreamWaitEvent(stream, ev_join, 0));
         }
     }
     if (d_post)
-        LAUNCH(K_FINAL, hipLaunchKernelGGL(k_finalize, g_cols, blk, 0, stream, c2v, prior, iters, d_col_ptr, d_col_edge,
-                                           d_post, msa, post_kind == LDPC_POST_RATIO ? 1 : 0, Bc, N, E));
+        LAUNCH(K_FINAL, hipLaunchKernelGGL(k_finalize, g_cols_all, blk, 0, stream, post_t, prior, iters, d_post, msa,
+                                           post_kind == LDPC_POST_RATIO ? 1 : 0, Bc, N));
     if (d_hard) {
         const int64_t nblk = Bc * ((N + 255) / 256);
         const unsigned grid = (unsigned)std::min<int64_t>(nblk, 1 << 20);

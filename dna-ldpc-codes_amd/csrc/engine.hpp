@@ -35,6 +35,13 @@ struct Engine {
     hipStream_t stream = nullptr;
     int64_t cap = 0;        // codewords per pass (multiple of 64)
     int64_t cap_tiles = 0;
+    int64_t group_tiles = 0;  // tiles per check/variable launch; c2v holds only one group
+    bool nt_d = false;        // nontemporal loads/stores of the v2c ("d") stream
+    bool pipe = false;        // check(g+1) on `stream` overlaps variable(g) on `stream2`
+    bool lr_csc = false;      // c2v scratch in column (CSC) order (regular kernels only)
+    int32_t* d_csc_pos = nullptr;  // [E] CSC position of CSR edge e
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_chk[2] = {nullptr, nullptr}, ev_var[2] = {nullptr, nullptr}, ev_join = nullptr;
     // graph on device
     int32_t* d_row_ptr = nullptr;
     int32_t* d_col_idx = nullptr;
@@ -49,15 +56,18 @@ struct Engine {
     uint64_t* active = nullptr;
     int32_t* iters = nullptr;
     uint8_t* valid = nullptr;
-    // profiling
-    bool profile = false;
+    double* post_t = nullptr;  // [tiles][N][64] per-iteration posterior (allocated on first use)
+    // profiling: HIP events around every `profile_stride`-th launch of a class
+    int profile_stride = 0;
+    int64_t sampled[K_NCLASS] = {0};
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_live[K_NCLASS];
     std::vector<hipEvent_t> ev_pool;
     int64_t launches[K_NCLASS] = {0};
     double ms[K_NCLASS] = {0};
 
     ~Engine();
-    int init(const HostGraph* graph, int dev, int algorithm, int64_t chunk);
+    int init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, int64_t group = -1, int nt = -1,
+             int pipelined = -1, int csc = -1);
     // decode Bc <= cap codewords whose [Bc][N] input is at d_in (device)
     int run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_iter, uint8_t* d_hard, double* d_post,
                   int post_kind, int32_t* d_iters, uint8_t* d_valid);
@@ -69,8 +79,10 @@ struct Engine {
 
   private:
     hipEvent_t get_event();
-    int mark_begin(KClass c, hipEvent_t* b);
-    int mark_end(KClass c, hipEvent_t b);
+    int mark_begin(KClass c, hipStream_t s, hipEvent_t* b);
+    int mark_end(KClass c, hipStream_t s, hipEvent_t b);
+    int launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt);
+    int launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt);
 };
 
 // bytes of device memory per resident codeword

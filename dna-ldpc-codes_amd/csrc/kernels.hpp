@@ -38,6 +38,20 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m)
     return ((uint64_t)hi << 32) | lo;
 }
 
+// streaming access to the v2c ("d") array, optionally nontemporal
+template <bool NT>
+__device__ __forceinline__ double ld(const double* p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(double* p, double v)
+{
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
 {
     x += 0x9E3779B97F4A7C15ull;
@@ -163,25 +177,29 @@ __global__ __launch_bounds__(1024) void k_syndrome(const uint64_t* __restrict__ 
 // -> identical values), which keeps the kernel at 2 waves/SIMD.
 // grid (ceil(M/4), tiles), block 256: one wave per (row, tile).
 // ---------------------------------------------------------------------------
-template <int DC>
+template <int DC, bool NT, bool CSCL>
 __global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ dmsg, double* __restrict__ lr,
-                                                  const uint64_t* __restrict__ active, int32_t M, int64_t E)
+                                                     const uint64_t* __restrict__ active,
+                                                     const int32_t* __restrict__ pos, int32_t M, int64_t E,
+                                                     int64_t t0)
 {
     constexpr int SEG = 8;
     constexpr int NSEG = (DC + SEG - 1) / SEG;
     const int lane = lane_id();
     const int32_t row = blockIdx.x * 4 + wave_id();
-    const int64_t t = blockIdx.y;
+    const int64_t t = t0 + blockIdx.y;
     if (row >= M) return;
     const uint64_t act = active[t];
     if (!((act >> lane) & 1ull)) return;
-    const size_t base = ((size_t)t * E + (size_t)row * DC) * TILE + lane;
-    const double* __restrict__ src = dmsg + base;
-    double* __restrict__ dst = lr + base;
+    const double* __restrict__ src = dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
+    // c2v scratch: CSR order (row-contiguous) or CSC order (column-contiguous,
+    // position pos[e]) so the variable phase reads each column contiguously
+    double* __restrict__ dst = lr + (size_t)blockIdx.y * E * TILE + lane;
+    const int32_t* __restrict__ prow = pos + (size_t)row * DC;
 
     double x[DC];
 #pragma unroll
-    for (int k = 0; k < DC; ++k) x[k] = src[(size_t)k * TILE];
+    for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
 
     double cp[NSEG];
     double p = 1.0;
@@ -208,7 +226,8 @@ __global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ 
             const int k = g * SEG + i;
             if (k < DC) {
                 const double tt = pk[i] * s;
-                dst[(size_t)k * TILE] = (1.0 + tt) / (1.0 - tt);
+                const size_t p = CSCL ? (size_t)prow[k] : (size_t)row * DC + k;
+                dst[p * TILE] = (1.0 + tt) / (1.0 - tt);
                 s = s * x[k];
             }
         }
@@ -219,28 +238,28 @@ __global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ 
 // the reference does (e->lr = dl in the forward pass, dec.cpp:650-653).
 __global__ __launch_bounds__(256) void k_check_bp_gen(const double* __restrict__ dmsg, double* __restrict__ lr,
                                                       const uint64_t* __restrict__ active,
-                                                      const int32_t* __restrict__ row_ptr, int32_t M, int64_t E)
+                                                      const int32_t* __restrict__ row_ptr, int32_t M, int64_t E,
+                                                      int64_t t0)
 {
     const int lane = lane_id();
     const int32_t row = blockIdx.x * 4 + wave_id();
-    const int64_t t = blockIdx.y;
+    const int64_t t = t0 + blockIdx.y;
     if (row >= M) return;
     const uint64_t act = active[t];
     if (!((act >> lane) & 1ull)) return;
     const int32_t a = row_ptr[row], b = row_ptr[row + 1];
-    const size_t tb = (size_t)t * E;
+    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
     double dl = 1.0;
     for (int32_t e = a; e < b; ++e) {
-        const size_t o = (tb + e) * TILE + lane;
-        lr[o] = dl;
-        dl = dl * dmsg[o];
+        lr[(tl + e) * TILE + lane] = dl;
+        dl = dl * dmsg[(tb + e) * TILE + lane];
     }
     dl = 1.0;
     for (int32_t e = b - 1; e >= a; --e) {
-        const size_t o = (tb + e) * TILE + lane;
+        const size_t o = (tl + e) * TILE + lane;
         const double tt = lr[o] * dl;
         lr[o] = (1.0 + tt) / (1.0 - tt);
-        dl = dl * dmsg[o];
+        dl = dl * dmsg[(tb + e) * TILE + lane];
     }
 }
 
@@ -251,17 +270,19 @@ __global__ __launch_bounds__(256) void k_check_bp_gen(const double* __restrict__
 //   backward acc = 1; s = DV-1..0: pr_s *= acc; NaN -> 1; acc *= lr_s
 // then stores d_s = 1 - 2/(1+pr_s) for the next check phase and the ballot of
 // the hard decisions.  Converged lanes keep their state untouched.
-// grid (ceil(N/4), tiles), block 256: one wave per (column, tile).
+// Tiles t0 .. t0+gridDim.y-1; lr is the group's scratch ([t - t0][E][64]).
+// post (optional) receives P, the posterior ratio of this iteration.
+// grid (ceil(N/4), group tiles), block 256: one wave per (column, tile).
 // ---------------------------------------------------------------------------
-template <int DV>
+template <int DV, bool NT, bool CSCL>
 __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, double* __restrict__ dmsg,
                                                 const double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                 const uint64_t* __restrict__ active, const int32_t* __restrict__ col_edge,
-                                                int32_t N, int64_t E)
+                                                double* __restrict__ post, int32_t N, int64_t E, int64_t t0)
 {
     const int lane = lane_id();
     const int32_t j = blockIdx.x * 4 + wave_id();
-    const int64_t t = blockIdx.y;
+    const int64_t t = t0 + blockIdx.y;
     if (j >= N) return;
     const uint64_t act = active[t];
     if (act == 0) return;
@@ -269,25 +290,27 @@ __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, d
     int32_t eid[DV];
 #pragma unroll
     for (int s = 0; s < DV; ++s) eid[s] = col_edge[(size_t)j * DV + s];
-    const size_t tb = (size_t)t * E;
+    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
     bool h = false;
     if (live) {
-        const double LR = prior[((size_t)t * N + j) * TILE + lane];
+        const size_t pj = ((size_t)t * N + j) * TILE + lane;
+        const double LR = prior[pj];
         double l[DV], pr[DV];
 #pragma unroll
-        for (int s = 0; s < DV; ++s) l[s] = lr[(tb + eid[s]) * TILE + lane];
+        for (int s = 0; s < DV; ++s) l[s] = lr[(tl + (CSCL ? (size_t)j * DV + s : (size_t)eid[s])) * TILE + lane];
         double p = LR;
 #pragma unroll
         for (int s = 0; s < DV; ++s) { pr[s] = p; p = p * l[s]; }
         if (__builtin_isnan(p)) p = 1.0;
         h = (p <= 1.0);
+        if (post) post[pj] = p;
         double acc = 1.0;
 #pragma unroll
         for (int s = DV - 1; s >= 0; --s) {
             double v = pr[s] * acc;
             if (__builtin_isnan(v)) v = 1.0;
             acc = acc * l[s];
-            dmsg[(tb + eid[s]) * TILE + lane] = 1.0 - 2.0 / (1.0 + v);
+            st<NT>(dmsg + (tb + eid[s]) * TILE + lane, 1.0 - 2.0 / (1.0 + v));
         }
     }
     const uint64_t m = __ballot(h);
@@ -303,33 +326,37 @@ __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, d
 __global__ __launch_bounds__(256) void k_var_bp_gen(const double* __restrict__ lr, double* __restrict__ dmsg,
                                                     const double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                     const uint64_t* __restrict__ active, const int32_t* __restrict__ col_ptr,
-                                                    const int32_t* __restrict__ col_edge, int32_t N, int64_t E)
+                                                    const int32_t* __restrict__ col_edge, double* __restrict__ post,
+                                                    int32_t N, int64_t E, int64_t t0)
 {
     const int lane = lane_id();
     const int32_t j = blockIdx.x * 4 + wave_id();
-    const int64_t t = blockIdx.y;
+    const int64_t t = t0 + blockIdx.y;
     if (j >= N) return;
     const uint64_t act = active[t];
     if (act == 0) return;
     const bool live = (act >> lane) & 1ull;
     const int32_t a = col_ptr[j], b = col_ptr[j + 1];
-    const size_t tb = (size_t)t * E;
+    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
     bool h = false;
     if (live) {
-        double p = prior[((size_t)t * N + j) * TILE + lane];
+        const size_t pj = ((size_t)t * N + j) * TILE + lane;
+        double p = prior[pj];
         for (int32_t q = a; q < b; ++q) {
-            const size_t o = (tb + col_edge[q]) * TILE + lane;
-            dmsg[o] = p;
-            p = p * lr[o];
+            const int32_t e = col_edge[q];
+            dmsg[(tb + e) * TILE + lane] = p;
+            p = p * lr[(tl + e) * TILE + lane];
         }
         if (__builtin_isnan(p)) p = 1.0;
         h = (p <= 1.0);
+        if (post) post[pj] = p;
         double acc = 1.0;
         for (int32_t q = b - 1; q >= a; --q) {
-            const size_t o = (tb + col_edge[q]) * TILE + lane;
+            const int32_t e = col_edge[q];
+            const size_t o = (tb + e) * TILE + lane;
             double v = dmsg[o] * acc;
             if (__builtin_isnan(v)) v = 1.0;
-            acc = acc * lr[o];
+            acc = acc * lr[(tl + e) * TILE + lane];
             dmsg[o] = 1.0 - 2.0 / (1.0 + v);
         }
     }
@@ -352,24 +379,26 @@ __global__ __launch_bounds__(256) void k_var_bp_gen(const double* __restrict__ l
 // (x >= 0 ? +1 : -1) (NaN counts -1).  c2v = (double)sign * mag.
 // dc == 1: mag stays -1 -> 0, sign 1 -> 0.0 (dec.cpp:1427-1430).
 // ---------------------------------------------------------------------------
-template <int DC>
+template <int DC, bool NT, bool CSCL>
 __global__ __launch_bounds__(256) void k_check_msa(const double* __restrict__ v2c, double* __restrict__ c2v,
-                                                   const uint64_t* __restrict__ active, int32_t M, int64_t E)
+                                                   const uint64_t* __restrict__ active,
+                                                   const int32_t* __restrict__ pos, int32_t M, int64_t E,
+                                                   int64_t t0)
 {
     const int lane = lane_id();
     const int32_t row = blockIdx.x * 4 + wave_id();
-    const int64_t t = blockIdx.y;
+    const int64_t t = t0 + blockIdx.y;
     if (row >= M) return;
     const uint64_t act = active[t];
     if (!((act >> lane) & 1ull)) return;
-    const size_t base = ((size_t)t * E + (size_t)row * DC) * TILE + lane;
-    const double* __restrict__ src = v2c + base;
-    double* __restrict__ dst = c2v + base;
+    const double* __restrict__ src = v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
+    double* __restrict__ dst = c2v + (size_t)blockIdx.y * E * TILE + lane;
+    const int32_t* __restrict__ prow = pos + (size_t)row * DC;
     double x[DC];
 #pragma unroll
-    for (int k = 0; k < DC; ++k) x[k] = src[(size_t)k * TILE];
+    for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
     if (DC == 1) {
-        dst[0] = 0.0;
+        dst[(CSCL ? (size_t)prow[0] : (size_t)row) * TILE] = 0.0;
         return;
     }
     double m1 = __builtin_inf(), m2 = __builtin_inf();
@@ -394,24 +423,26 @@ __global__ __launch_bounds__(256) void k_check_msa(const double* __restrict__ v2
         if (__builtin_isnan(af)) mag = af;
         const uint32_t nk = (x[k] >= 0) ? 0u : 1u;
         const int sign = ((neg ^ nk) & 1u) ? -1 : 1;
-        dst[(size_t)k * TILE] = (double)sign * mag;
+        const size_t p = CSCL ? (size_t)prow[k] : (size_t)row * DC + k;
+        dst[p * TILE] = (double)sign * mag;
     }
 }
 
 __global__ __launch_bounds__(256) void k_check_msa_gen(const double* __restrict__ v2c, double* __restrict__ c2v,
                                                        const uint64_t* __restrict__ active,
-                                                       const int32_t* __restrict__ row_ptr, int32_t M, int64_t E)
+                                                       const int32_t* __restrict__ row_ptr, int32_t M, int64_t E,
+                                                       int64_t t0)
 {
     const int lane = lane_id();
     const int32_t row = blockIdx.x * 4 + wave_id();
-    const int64_t t = blockIdx.y;
+    const int64_t t = t0 + blockIdx.y;
     if (row >= M) return;
     const uint64_t act = active[t];
     if (!((act >> lane) & 1ull)) return;
     const int32_t a = row_ptr[row], b = row_ptr[row + 1];
-    const size_t tb = (size_t)t * E;
+    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
     if (b - a == 0) return;
-    if (b - a == 1) { c2v[(tb + a) * TILE + lane] = 0.0; return; }
+    if (b - a == 1) { c2v[(tl + a) * TILE + lane] = 0.0; return; }
     double m1 = __builtin_inf(), m2 = __builtin_inf();
     int32_t i1 = -1;
     uint32_t neg = 0;
@@ -428,14 +459,13 @@ __global__ __launch_bounds__(256) void k_check_msa_gen(const double* __restrict_
     const double a0 = __builtin_fabs(v2c[(tb + a) * TILE + lane]);
     const double a1 = __builtin_fabs(v2c[(tb + a + 1) * TILE + lane]);
     for (int32_t e = a; e < b; ++e) {
-        const size_t o = (tb + e) * TILE + lane;
-        const double xv = v2c[o];
+        const double xv = v2c[(tb + e) * TILE + lane];
         const double af = (e == a) ? a1 : a0;
         double mag = (e == i1) ? m2 : m1;
         if (__builtin_isnan(af)) mag = af;
         const uint32_t nk = (xv >= 0) ? 0u : 1u;
         const int sign = ((neg ^ nk) & 1u) ? -1 : 1;
-        c2v[o] = (double)sign * mag;
+        c2v[(tl + e) * TILE + lane] = (double)sign * mag;
     }
 }
 
@@ -443,17 +473,17 @@ __global__ __launch_bounds__(256) void k_check_msa_gen(const double* __restrict_
 // Min-sum variable-node phase + decision (Variable_Update_MSA_INF
 // dec.cpp:1597-1619, Decision_MSA_INF dec.cpp:1659-1678):
 //   v2c_s = ((LLR + c_0) + c_1) ... skipping c_s, ascending row order
-//   L = LLR + c_0 + ... + c_{DV-1};  dblk = !(L > 0)
+//   L = LLR + c_0 + ... + c_{DV-1};  dblk = !(L > 0);  post (optional) <- L
 // ---------------------------------------------------------------------------
-template <int DV>
+template <int DV, bool NT, bool CSCL>
 __global__ __launch_bounds__(256) void k_var_msa(const double* __restrict__ c2v, double* __restrict__ v2c,
                                                  const double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                  const uint64_t* __restrict__ active, const int32_t* __restrict__ col_edge,
-                                                 int32_t N, int64_t E)
+                                                 double* __restrict__ post, int32_t N, int64_t E, int64_t t0)
 {
     const int lane = lane_id();
     const int32_t j = blockIdx.x * 4 + wave_id();
-    const int64_t t = blockIdx.y;
+    const int64_t t = t0 + blockIdx.y;
     if (j >= N) return;
     const uint64_t act = active[t];
     if (act == 0) return;
@@ -461,25 +491,27 @@ __global__ __launch_bounds__(256) void k_var_msa(const double* __restrict__ c2v,
     int32_t eid[DV];
 #pragma unroll
     for (int s = 0; s < DV; ++s) eid[s] = col_edge[(size_t)j * DV + s];
-    const size_t tb = (size_t)t * E;
+    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
     bool h = false;
     if (live) {
-        const double llr = prior[((size_t)t * N + j) * TILE + lane];
+        const size_t pj = ((size_t)t * N + j) * TILE + lane;
+        const double llr = prior[pj];
         double c[DV];
 #pragma unroll
-        for (int s = 0; s < DV; ++s) c[s] = c2v[(tb + eid[s]) * TILE + lane];
+        for (int s = 0; s < DV; ++s) c[s] = c2v[(tl + (CSCL ? (size_t)j * DV + s : (size_t)eid[s])) * TILE + lane];
 #pragma unroll
         for (int s = 0; s < DV; ++s) {
             double sum = llr;
 #pragma unroll
             for (int r = 0; r < DV; ++r)
                 if (r != s) sum = sum + c[r];
-            v2c[(tb + eid[s]) * TILE + lane] = sum;
+            st<NT>(v2c + (tb + eid[s]) * TILE + lane, sum);
         }
         double L = llr;
 #pragma unroll
         for (int s = 0; s < DV; ++s) L = L + c[s];
         h = !(L > 0);
+        if (post) post[pj] = L;
     }
     const uint64_t m = __ballot(h);
     if (lane == 0) {
@@ -492,30 +524,33 @@ __global__ __launch_bounds__(256) void k_var_msa(const double* __restrict__ c2v,
 __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ c2v, double* __restrict__ v2c,
                                                      const double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                      const uint64_t* __restrict__ active, const int32_t* __restrict__ col_ptr,
-                                                     const int32_t* __restrict__ col_edge, int32_t N, int64_t E)
+                                                     const int32_t* __restrict__ col_edge, double* __restrict__ post,
+                                                     int32_t N, int64_t E, int64_t t0)
 {
     const int lane = lane_id();
     const int32_t j = blockIdx.x * 4 + wave_id();
-    const int64_t t = blockIdx.y;
+    const int64_t t = t0 + blockIdx.y;
     if (j >= N) return;
     const uint64_t act = active[t];
     if (act == 0) return;
     const bool live = (act >> lane) & 1ull;
     const int32_t a = col_ptr[j], b = col_ptr[j + 1];
-    const size_t tb = (size_t)t * E;
+    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
     bool h = false;
     if (live) {
-        const double llr = prior[((size_t)t * N + j) * TILE + lane];
+        const size_t pj = ((size_t)t * N + j) * TILE + lane;
+        const double llr = prior[pj];
         // v2c is written only after all sums are formed, c2v is read-only here
         for (int32_t s = a; s < b; ++s) {
             double sum = llr;
             for (int32_t r = a; r < b; ++r)
-                if (r != s) sum = sum + c2v[(tb + col_edge[r]) * TILE + lane];
+                if (r != s) sum = sum + c2v[(tl + col_edge[r]) * TILE + lane];
             v2c[(tb + col_edge[s]) * TILE + lane] = sum;
         }
         double L = llr;
-        for (int32_t s = a; s < b; ++s) L = L + c2v[(tb + col_edge[s]) * TILE + lane];
+        for (int32_t s = a; s < b; ++s) L = L + c2v[(tl + col_edge[s]) * TILE + lane];
         h = !(L > 0);
+        if (post) post[pj] = L;
     }
     const uint64_t m = __ballot(h);
     if (lane == 0) {
@@ -526,16 +561,18 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// finalize: posterior per codeword/bit, written row-major [b][N].
+// finalize: posterior per codeword/bit, written row-major [b][N].  The
+// variable phase leaves the posterior of its iteration in post_t ([t][N][64]):
 //   BP : P = LR * prod lr (ascending row, dec.cpp:669-674), NaN -> 1
 //        (dec.cpp:676-677); iters == 0 -> P = LR (lr still 1 from init).
-//        post = log(P) (LDPC_POST_LLR) or P (LDPC_POST_RATIO).
+//        out = log(P) (LDPC_POST_LLR) or P (LDPC_POST_RATIO).
 //   MSA: L = LLR + sum c2v (Decision_MSA_INF order); iters == 0 -> LLR.
+// A codeword that stopped at iteration n > 0 was last updated by variable
+// phase n-1, so post_t holds exactly its exit posterior.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ c2v, const double* __restrict__ prior,
-                                                  const int32_t* __restrict__ iters, const int32_t* __restrict__ col_ptr,
-                                                  const int32_t* __restrict__ col_edge, double* __restrict__ post,
-                                                  int algo_msa, int post_ratio, int64_t Bc, int32_t N, int64_t E)
+__global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ post_t, const double* __restrict__ prior,
+                                                  const int32_t* __restrict__ iters, double* __restrict__ post,
+                                                  int algo_msa, int post_ratio, int64_t Bc, int32_t N)
 {
     const int lane = lane_id();
     const int32_t j = blockIdx.x * 4 + wave_id();
@@ -543,20 +580,12 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ c2v
     if (j >= N) return;
     const int64_t b = t * TILE + lane;
     if (b >= Bc) return;
-    const double pv = prior[((size_t)t * N + j) * TILE + lane];
-    const bool ran = iters[b] > 0;
-    const int32_t a = col_ptr[j], e1 = col_ptr[j + 1];
-    const size_t tb = (size_t)t * E;
+    const size_t pj = ((size_t)t * N + j) * TILE + lane;
     double out;
     if (algo_msa) {
-        double L = pv;
-        if (ran)
-            for (int32_t q = a; q < e1; ++q) L = L + c2v[(tb + col_edge[q]) * TILE + lane];
-        out = L;
+        out = iters[b] > 0 ? post_t[pj] : prior[pj];
     } else {
-        double P = pv;
-        if (ran)
-            for (int32_t q = a; q < e1; ++q) P = P * c2v[(tb + col_edge[q]) * TILE + lane];
+        double P = iters[b] > 0 ? post_t[pj] : prior[pj];
         if (__builtin_isnan(P)) P = 1.0;
         out = post_ratio ? P : log(P);
     }

@@ -51,8 +51,7 @@ class Opts(C.Structure):
 
 
 class KernelStats(C.Structure):
-    _fields_ = [("launches", C.c_int64 * 6), ("ms", C.c_double * 6), ("edge_iters", C.c_int64),
-                ("cw_iters", C.c_int64)]
+    _fields_ = [("launches", C.c_int64 * 6), ("sampled", C.c_int64 * 6), ("ms", C.c_double * 6)]
 
 
 KCLASS = ("check", "variable", "syndrome", "init", "finalize", "other")
@@ -63,7 +62,7 @@ _lib_lock = threading.Lock()
 EXPORTS = [
     "ldpc_abi_version", "ldpc_last_error", "ldpc_device_count", "ldpc_graph_load", "ldpc_graph_from_edges",
     "ldpc_graph_free", "ldpc_graph_info", "ldpc_graph_edges", "ldpc_graph_syndrome", "ldpc_decode",
-    "ldpc_engine_create", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
+    "ldpc_engine_create", "ldpc_engine_create_ex", "ldpc_engine_info", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
     "ldpc_engine_gen_bsc", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
     "ldpc_dev_memcpy",
 ]
@@ -96,6 +95,9 @@ def lib():
         L.ldpc_decode.argtypes = [vp, vp, i64, i32, i32, vp, vp, vp, vp, C.POINTER(Opts)]
         L.ldpc_engine_create.argtypes = [vp, i32, i32, i64, pint]
         L.ldpc_engine_create.restype = vp
+        L.ldpc_engine_create_ex.argtypes = [vp, i32, i32, i64, i64, i32, pint]
+        L.ldpc_engine_create_ex.restype = vp
+        L.ldpc_engine_info.argtypes = [vp, vp, vp, vp]
         L.ldpc_engine_free.argtypes = [vp]
         L.ldpc_engine_free.restype = None
         L.ldpc_engine_decode.argtypes = [vp, vp, i32, i64, i32, vp, vp, i32, vp, vp]
@@ -355,12 +357,22 @@ class DeviceBuffer:
 
 
 class Engine:
-    def __init__(self, g: Graph, device: int = 0, algo="bp", chunk: int = 0):
+    def __init__(self, g: Graph, device: int = 0, algo="bp", chunk: int = 0, group_tiles: int = -1,
+                 nontemporal: Optional[bool] = None, pipeline: Optional[bool] = None,
+                 csc_scratch: Optional[bool] = None):
         self.g, self.device, self.algo = g, device, _algo(algo)
         err = C.c_int(0)
-        self._h = lib().ldpc_engine_create(g.handle, device, self.algo, chunk, C.byref(err))
+        if nontemporal is None and pipeline is None and csc_scratch is None:
+            flags = -1
+        else:
+            flags = int(bool(nontemporal)) | (int(bool(pipeline)) << 1) | (int(bool(csc_scratch)) << 2)
+        self._h = lib().ldpc_engine_create_ex(g.handle, device, self.algo, chunk, group_tiles, flags, C.byref(err))
         if not self._h:
             raise LdpcError(err.value, (lib().ldpc_last_error() or b"").decode())
+        cap, grp, fl = C.c_int64(), C.c_int64(), C.c_int32()
+        _check(lib().ldpc_engine_info(self._h, C.byref(cap), C.byref(grp), C.byref(fl)))
+        self.cap, self.group_tiles = cap.value, grp.value
+        self.nontemporal, self.pipeline, self.csc_scratch = bool(fl.value & 1), bool(fl.value & 2), bool(fl.value & 4)
 
     def decode(self, d_in, in_kind: int, B: int, max_iter: int, d_hard=None, d_post=None, post_kind=POST_LLR,
                d_iters=None, d_valid=None):
@@ -373,13 +385,15 @@ class Engine:
     def sync(self):
         _check(lib().ldpc_engine_sync(self._h))
 
-    def profile(self, enable: bool):
-        _check(lib().ldpc_engine_profile(self._h, 1 if enable else 0))
+    def profile(self, stride: int):
+        """HIP-event timing of every `stride`-th launch per kernel class (0: off)."""
+        _check(lib().ldpc_engine_profile(self._h, int(stride)))
 
     def stats(self) -> dict:
         s = KernelStats()
         _check(lib().ldpc_engine_stats(self._h, C.byref(s)))
-        return {k: {"launches": int(s.launches[i]), "ms": float(s.ms[i])} for i, k in enumerate(KCLASS)}
+        return {k: {"launches": int(s.launches[i]), "sampled": int(s.sampled[i]), "ms": float(s.ms[i])}
+                for i, k in enumerate(KCLASS)}
 
     def close(self):
         if getattr(self, "_h", None):

@@ -124,6 +124,16 @@ typedef struct ldpc_engine ldpc_engine;
 
 /* One engine = one device + one HIP stream + chunk-sized message buffers. */
 ldpc_engine *ldpc_engine_create(const ldpc_graph *g, int32_t device, int32_t algo, int64_t chunk, int *err);
+
+/* Same with the schedule knobs: group_tiles = 64-codeword tiles per
+ * check/variable launch (the check->variable messages of one group stay
+ * resident in the Infinity Cache; 0 = whole pass, -1 = default / env
+ * LDPC_GROUP_TILES); flags bit 0 = nontemporal v2c stream, bit 1 = overlap
+ * check(g+1) with variable(g) on a second stream, bit 2 = check->variable
+ * messages stored in column order (flags -1 = defaults / env LDPC_NT_D,
+ * LDPC_PIPE, LDPC_LR_CSC). */
+ldpc_engine *ldpc_engine_create_ex(const ldpc_graph *g, int32_t device, int32_t algo, int64_t chunk,
+                                   int64_t group_tiles, int32_t flags, int *err);
 void ldpc_engine_free(ldpc_engine *e);
 
 /* Decode B codewords whose input already lives in device memory (d_in:
@@ -147,16 +157,20 @@ void *ldpc_engine_stream(ldpc_engine *e);
 int ldpc_engine_gen_bsc(ldpc_engine *e, double *d_out, int32_t out_kind, int64_t b0, int64_t B,
                         const uint8_t *d_codewords, int32_t n_cw, uint64_t seed, double p, double llr_mag);
 
-/* Kernel timing (HIP events on the engine stream around every launch of
- * each kernel class) -- enable before, read after ldpc_engine_sync(). */
+/* Kernel timing: HIP events on the engine stream around every stride-th
+ * launch of each kernel class (stride 1 = every launch, 0 = off).  Enabling
+ * resets the counters; read them after ldpc_engine_sync(). */
 typedef struct ldpc_kernel_stats {
     int64_t launches[6];    /* [0]=check [1]=variable [2]=syndrome [3]=init [4]=finalize [5]=other */
-    double ms[6];           /* summed device time per class */
-    int64_t edge_iters;     /* sum over launches of (live tiles * 64 * E) for check+variable */
-    int64_t cw_iters;       /* codeword-iterations executed (sum of iters) */
+    int64_t sampled[6];     /* launches that carried events */
+    double ms[6];           /* summed device time of the sampled launches */
 } ldpc_kernel_stats;
 
-int ldpc_engine_profile(ldpc_engine *e, int32_t enable);
+int ldpc_engine_profile(ldpc_engine *e, int32_t stride);
+
+/* The schedule an engine runs with: group tiles, nontemporal flag, resident
+ * codewords per pass. */
+int ldpc_engine_info(ldpc_engine *e, int64_t *cap, int64_t *group_tiles, int32_t *flags);
 int ldpc_engine_stats(ldpc_engine *e, ldpc_kernel_stats *out);
 
 /* Device buffers for callers without their own HIP allocator (bench, tests). */
