@@ -21,6 +21,7 @@ max elapsed.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import math
 import os
@@ -157,10 +158,21 @@ def main():
     achieved = bytes_per_launch / (k_avg * 1e-3) / 1e9 if k_avg > 0 else None
     it_ms = sum(avg_ms(k) * st[k]["launches"] for k in ("check", "variable", "syndrome"))
     iter_bytes = (32.0 * E + 10.0 * N) * cw_iters
+    # traffic: HBM bytes per codeword-iteration of this kernel from the committed
+    # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE), scaled to this launch size
+    kname = f"k_{'check' if dom == 'check' else 'var'}_{algo}"
+    traffic, traffic_src = None, None
+    for tf in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
+        tj = json.load(open(tf))
+        if kname in tj.get("per_cw_iter", {}):
+            traffic = round(tj["per_cw_iter"][kname] * cw_iters / k_launch)
+            traffic_src = os.path.relpath(tf, ROOT)
+            break
     roof = {
-        "bound": "hbm", "kernel": f"k_{'check' if dom == 'check' else 'var'}_{algo}",
+        "bound": "hbm", "kernel": kname,
         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": None,
+        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,
+        "traffic_source": traffic_src,
         "bytes_per_launch": round(bytes_per_launch), "avg_launch_ms": round(k_avg, 4),
         "iteration_GBps": round(iter_bytes / (it_ms * 1e-3) / 1e9, 1) if it_ms > 0 else None,
         "avg_ms": {k: round(avg_ms(k), 4) for k in st},

@@ -1,0 +1,111 @@
+"""In-process LDPC stage of the DNA-storage decoder.
+
+Reproduces the decode loop of the reference's ex_decoder/decoder.py without
+the 272+ `ldpc.exe` processes and soft/dec text files:
+
+* first decode (decoder.py:553-581): every codeword's LLR vector decoded with
+  max_iter 200; the genie check against the true codeword gives `fail_DNA`
+  (1-based indices) and the per-strand `re_decode` counts (output bit !=
+  input hard decision), from which `erasure_index` = strands with > 140
+  (decoder.py:590, def_func.re_index);
+* second decode (decoder.py:592-664): while failures remain and eps2 > 0.001,
+  rescale the ORIGINAL LLRs of the failed codewords by
+  ``(x * ln((1-eps2+0.0005)/(eps2-0.0005))) / ln((1-eps)/eps)`` (zeros kept),
+  lower eps2 by 0.0005 and re-decode.  The reference resets ``fail_DNA2 = []``
+  inside its per-codeword loop (decoder.py:659-661), so only the LAST re-decoded
+  codeword's outcome survives an iteration; this module keeps that behaviour
+  (``faithful=True``, the default) or tracks every failure (``faithful=False``).
+
+All decodes of one stage go to the GPU in ONE batched call.  `decode_fn` is
+injectable so tests can run the identical flow on the CPU oracle.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+
+DecodeFn = Callable[[np.ndarray, int], np.ndarray]  # (llr [B][N], max_iter) -> hard [B][N]
+
+
+def gpu_decode_fn(graph=None, algo="bp") -> DecodeFn:
+    import ldpc_amd
+    g = graph if graph is not None else ldpc_amd.graph(ldpc_amd.default_pchk())
+
+    def fn(llr: np.ndarray, max_iter: int) -> np.ndarray:
+        hard, _, _, _ = g.decode(llr, max_iter=max_iter, algo=algo, post=None)
+        return hard
+
+    return fn
+
+
+def rescale(llr: np.ndarray, eps: float, eps2: float) -> np.ndarray:
+    """decoder.py:603-609: x -> x * ln((1-eps2+.0005)/(eps2-.0005)) / ln((1-eps)/eps), 0 kept."""
+    num = math.log((1 - eps2 + 0.0005) / (eps2 - 0.0005))
+    den = math.log((1 - eps) / eps)
+    return np.where(llr == 0, llr, (llr * num) / den)
+
+
+def decode_trial(llr: np.ndarray, codewords: np.ndarray, eps: float = 0.02, max_iter: int = 200,
+                 decode_fn: Optional[DecodeFn] = None, faithful: bool = True) -> Dict:
+    """Run the LDPC part of one decoder.py trial.  llr: [n_cw][N] (row i = soft
+    file i+1), codewords: [n_cw][N] true codewords (the genie)."""
+    decode_fn = decode_fn or gpu_decode_fn()
+    llr = np.ascontiguousarray(llr, dtype=np.float64)
+    n_cw, N = llr.shape
+    t0 = time.perf_counter()
+    hard = decode_fn(llr, max_iter)
+    t_first = time.perf_counter() - t0
+    errors = (hard != codewords).sum(axis=1)
+    fail = [i + 1 for i in range(n_cw) if errors[i] != 0]
+    re_decode = (hard != (llr < 0)).sum(axis=0)  # decoder.py:565-574
+    erasure_index = [j for j in range(N) if re_decode[j] > 140]
+
+    fail2: List[int] = list(fail)
+    iter_sec = 0
+    eps2 = eps - 0.0005
+    second_errors = {}
+    t1 = time.perf_counter()
+    while fail2 and eps2 > 0.001:
+        iter_sec += 1
+        batch = np.stack([rescale(llr[i - 1], eps, eps2) for i in fail2])
+        eps2 = eps2 - 0.0005
+        h2 = decode_fn(batch, max_iter)
+        new: List[int] = []
+        for k, i in enumerate(fail2):
+            v = int((h2[k] != codewords[i - 1]).sum())
+            second_errors[i] = v
+            if faithful:
+                new = []  # decoder.py:659-661 resets the list per codeword
+            if v != 0:
+                new.append(i)
+            if v == 0:
+                hard[i - 1] = h2[k]
+        fail2 = new
+    t_second = time.perf_counter() - t1
+    return {
+        "first_success": n_cw - len(fail), "second_success": n_cw - len(fail2), "n": n_cw,
+        "fail_first": fail, "fail_second": fail2, "second_iterations": iter_sec,
+        "first_errors": {i: int(errors[i - 1]) for i in fail}, "second_errors": second_errors,
+        "erasure_index": erasure_index, "hard": hard, "t_first_s": t_first, "t_second_s": t_second,
+    }
+
+
+def report(res: Dict, rs: int = 72000) -> str:
+    """The o_/x_ result-file body (decoder.py:668-727) without the wall time."""
+    n = res["n"]
+    ok = not res["fail_second"]
+    fmt = lambda xs: ("None" if not xs else " ".join(str(v) for v in xs) + " ")  # noqa: E731
+    lines = ["=" * 78, " " * 31 + "Results" + " " * 40, "=" * 78, f"Random Sampling Number: {rs}"]
+    if ok:
+        lines += ["Decoding success", "", "First decoding result:   %d/%d" % (res["first_success"], n),
+                  "Second decoding result:  %d/%d" % (res["second_success"], n),
+                  "Second decoding iteration number:  %d" % res["second_iterations"]]
+    else:
+        lines += ["Decoding failure", "", "First decoding result:\t%d/%d" % (res["first_success"], n),
+                  "Second decoding result:\t%d/%d" % (res["second_success"], n)]
+    lines += ["First decoding failure index: " + fmt(res["fail_first"]),
+              "Second decoding failure index: " + fmt(res["fail_second"])]
+    return "\n".join(lines) + "\n"
