@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--group-tiles", type=int, default=-1, help="tiles per check/variable launch (-1: engine default)")
     ap.add_argument("--nt", type=int, default=-1, help="nontemporal d-stream (-1: engine default)")
     ap.add_argument("--pipe", type=int, default=-1, help="two-stream check/variable overlap (-1: engine default)")
+    ap.add_argument("--cont", type=int, default=-1, help="continuous batching / lane refill (-1: engine default)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
     return ap.parse_args()
 
@@ -100,7 +101,8 @@ def main():
     dev = local
     algo = args.algo
     eng = L.Engine(G, dev, algo, chunk=args.chunk, group_tiles=args.group_tiles,
-                   nontemporal=None if args.nt < 0 else bool(args.nt), pipeline=None if args.pipe < 0 else bool(args.pipe))
+                   nontemporal=None if args.nt < 0 else bool(args.nt), pipeline=None if args.pipe < 0 else bool(args.pipe),
+                   continuous=None if args.cont < 0 else bool(args.cont))
     cw = synth.load_codewords()
     d_cw = L.DeviceBuffer(dev, cw.nbytes)
     d_cw.upload(cw)
@@ -188,7 +190,7 @@ def main():
                    "batch_per_gpu": B, "global_batch": int(total_cw / args.steps), "max_iter": args.max_iter,
                    "algo": algo, "parallelism": f"dp{world} (contiguous codeword shards, no collective)",
                    "resident_per_pass": eng.cap, "group_tiles": eng.group_tiles, "nontemporal_d": eng.nontemporal,
-                   "two_stream": eng.pipeline,
+                   "two_stream": eng.pipeline, "continuous": eng.continuous,
                    "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 4)},
         "roofline": roof,
     }

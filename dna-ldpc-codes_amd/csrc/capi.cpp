@@ -249,7 +249,7 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
             auto step = [&]() -> int {
                 LDPC_HIP(hipSetDevice(dev));
                 LDPC_HIP(hipMemcpyAsync(slot->d_in, slot->h_in, (size_t)Bc * N * 8, hipMemcpyHostToDevice, E.stream));
-                int r = E.run_chunk(slot->d_in, in_kind, Bc, max_iter, slot->d_hard, post_out ? slot->d_post : nullptr,
+                int r = E.decode(slot->d_in, in_kind, Bc, max_iter, slot->d_hard, post_out ? slot->d_post : nullptr,
                                     o.post_kind, slot->d_iters, slot->d_valid);
                 if (r) return r;
                 LDPC_HIP(hipMemcpyAsync(slot->h_hard, slot->d_hard, (size_t)Bc * N, hipMemcpyDeviceToHost, E.stream));
@@ -284,13 +284,13 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
 }
 
 ldpc_engine* ldpc_engine_create_ex(const ldpc_graph* g, int32_t device, int32_t algo, int64_t chunk,
-                                   int64_t group_tiles, int32_t flags, int* err)
+                                   int64_t group_tiles, int32_t flags_set, int32_t flags, int* err)
 {
+    auto bit = [&](int b) { return ((flags_set >> b) & 1) ? ((flags >> b) & 1) : -1; };
     if (!g) { set_error("null graph"); fail(LDPC_ERR_ARG, err); return nullptr; }
     auto e = std::make_unique<ldpc_engine>();
     e->e = std::make_unique<Engine>();
-    int rc = e->e->init(&g->h, device, algo, chunk, group_tiles, flags < 0 ? -1 : (flags & 1),
-                        flags < 0 ? -1 : ((flags >> 1) & 1), flags < 0 ? -1 : ((flags >> 2) & 1));
+    int rc = e->e->init(&g->h, device, algo, chunk, group_tiles, bit(0), bit(1), bit(2), bit(3));
     if (rc) { fail(rc, err); return nullptr; }
     if (err) *err = LDPC_OK;
     return e.release();
@@ -298,7 +298,7 @@ ldpc_engine* ldpc_engine_create_ex(const ldpc_graph* g, int32_t device, int32_t 
 
 ldpc_engine* ldpc_engine_create(const ldpc_graph* g, int32_t device, int32_t algo, int64_t chunk, int* err)
 {
-    return ldpc_engine_create_ex(g, device, algo, chunk, -1, -1, err);
+    return ldpc_engine_create_ex(g, device, algo, chunk, -1, 0, 0, err);
 }
 
 int ldpc_engine_info(ldpc_engine* e, int64_t* cap, int64_t* group_tiles, int32_t* flags)
@@ -306,7 +306,7 @@ int ldpc_engine_info(ldpc_engine* e, int64_t* cap, int64_t* group_tiles, int32_t
     if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
     if (cap) *cap = e->e->cap;
     if (group_tiles) *group_tiles = e->e->group_tiles;
-    if (flags) *flags = (e->e->nt_d ? 1 : 0) | (e->e->pipe ? 2 : 0) | (e->e->lr_csc ? 4 : 0);
+    if (flags) *flags = (e->e->nt_d ? 1 : 0) | (e->e->pipe ? 2 : 0) | (e->e->lr_csc ? 4 : 0) | (e->e->cont ? 8 : 0);
     return LDPC_OK;
 }
 

@@ -34,6 +34,7 @@ constexpr int64_t kDefaultGroupTiles = 3;  // tools/sweep.py on MI355X (DESIGN.m
 constexpr int64_t kDefaultNT = 1;
 constexpr int64_t kDefaultPipe = 0;
 constexpr int64_t kDefaultCsc = 0;
+constexpr int64_t kDefaultCont = 1;
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
@@ -59,6 +60,10 @@ Engine::~Engine()
         for (auto& p : ev_live[c]) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
     for (auto e : ev_pool) hipEventDestroy(e);
     hipFree(d_csc_pos);
+    hipFree(d_fresh); hipFree(d_occ); hipFree(d_lane_b); hipFree(d_lane_n); hipFree(d_ctr);
+    if (h_occ) hipHostFree(h_occ);
+    for (int i = 0; i < kRing; i++)
+        if (ev_ring[i]) hipEventDestroy(ev_ring[i]);
     hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge);
     hipFree(v2c); hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
     hipFree(post_t);
@@ -82,7 +87,7 @@ static int64_t env_int(const char* name, int64_t dflt)
 }
 
 int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, int64_t group, int nt, int pipelined,
-                 int csc)
+                 int csc, int cont_mode)
 {
     g = graph;
     device = dev;
@@ -135,6 +140,17 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         std::vector<int32_t> pos((size_t)std::max<int64_t>(g->E, 1), 0);
         for (size_t q = 0; q < g->col_edge.size(); q++) pos[(size_t)g->col_edge[q]] = (int32_t)q;
         if ((rc = upload(&d_csc_pos, pos))) return rc;
+    }
+    if (cont_mode < 0) cont_mode = (int)env_int("LDPC_CONT", kDefaultCont);
+    cont = cont_mode != 0 && g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
+    if (cont) {
+        LDPC_HIP(hipMalloc((void**)&d_fresh, (size_t)cap_tiles * sizeof(uint64_t)));
+        LDPC_HIP(hipMalloc((void**)&d_occ, (size_t)cap_tiles * sizeof(uint64_t)));
+        LDPC_HIP(hipMalloc((void**)&d_lane_b, (size_t)cap * sizeof(int64_t)));
+        LDPC_HIP(hipMalloc((void**)&d_lane_n, (size_t)cap * sizeof(int32_t)));
+        LDPC_HIP(hipMalloc((void**)&d_ctr, (size_t)(1 + kRing) * sizeof(unsigned long long)));
+        LDPC_HIP(hipHostMalloc((void**)&h_occ, (size_t)kRing * sizeof(unsigned long long), hipHostMallocDefault));
+        for (int i = 0; i < kRing; i++) LDPC_HIP(hipEventCreateWithFlags(&ev_ring[i], hipEventDisableTiming));
     }
     if (csc < 0) csc = (int)env_int("LDPC_LR_CSC", kDefaultCsc);
     lr_csc = csc != 0 && g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
@@ -221,18 +237,27 @@ static void check_regular(int algo, hipStream_t s, dim3 grid, const double* v2c,
         hipLaunchKernelGGL((k_check_msa<72, NT, CSCL>), grid, dim3(256), 0, s, v2c, scratch, active, pos, M, E, t0);
 }
 
-template <bool NT, bool CSCL>
-static void var_regular(int algo, hipStream_t s, dim3 grid, const double* scratch, double* v2c, const double* prior,
-                        uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N,
-                        int64_t E, int64_t t0)
+template <bool NT, bool CSCL, bool CONT>
+static void var_regular3(int algo, hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior,
+                         uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N,
+                         int64_t E, int64_t t0, const dev::Refill& rf)
 {
     using namespace dev;
     if (algo == LDPC_ALGO_BP)
-        hipLaunchKernelGGL((k_var_bp<8, NT, CSCL>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active, col_edge,
-                           pt, N, E, t0);
+        hipLaunchKernelGGL((k_var_bp<8, NT, CSCL, CONT>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
+                           col_edge, pt, N, E, t0, rf);
     else
-        hipLaunchKernelGGL((k_var_msa<8, NT, CSCL>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active, col_edge,
-                           pt, N, E, t0);
+        hipLaunchKernelGGL((k_var_msa<8, NT, CSCL, CONT>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
+                           col_edge, pt, N, E, t0, rf);
+}
+
+template <bool NT, bool CSCL>
+static void var_regular(int algo, hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior,
+                        uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N,
+                        int64_t E, int64_t t0, const dev::Refill& rf)
+{
+    if (rf.fresh) var_regular3<NT, CSCL, true>(algo, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+    else var_regular3<NT, CSCL, false>(algo, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
 }
 
 int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt)
@@ -258,7 +283,7 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
 }
 
 // variable phase (+ hard decisions, optional posterior) of tiles t0 .. t0+gt-1
-int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt)
+int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt, const dev::Refill& rf)
 {
     using namespace dev;
     const int32_t N = g->N;
@@ -268,10 +293,10 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
     if (reg8) {
         // lr_csc implies both phases use the regular kernels
         LAUNCH_ON(s, K_VAR, {
-            if (nt_d && lr_csc) var_regular<true, true>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0);
-            else if (nt_d) var_regular<true, false>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0);
-            else if (lr_csc) var_regular<false, true>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0);
-            else var_regular<false, false>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0);
+            if (nt_d && lr_csc) var_regular<true, true>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf);
+            else if (nt_d) var_regular<true, false>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf);
+            else if (lr_csc) var_regular<false, true>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf);
+            else var_regular<false, false>(algo, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf);
         });
     } else if (algo == LDPC_ALGO_BP) {
         LAUNCH_ON(s, K_VAR, hipLaunchKernelGGL(k_var_bp_gen, grid, blk, 0, s, scratch, v2c, prior, hard, active, d_col_ptr, d_col_edge, pt, N, E, t0));
@@ -321,14 +346,14 @@ int Engine::run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_i
             int rc;
             if (!pipe) {
                 if ((rc = launch_check(stream, scratch, t0, gt))) return rc;
-                if ((rc = launch_var(stream, scratch, t0, gt, pt))) return rc;
+                if ((rc = launch_var(stream, scratch, t0, gt, pt, dev::Refill{}))) return rc;
                 continue;
             }
             if (gi >= 2) LDPC_HIP(hipStreamWaitEvent(stream, ev_var[slot], 0));  // slot free again
             if ((rc = launch_check(stream, scratch, t0, gt))) return rc;
             LDPC_HIP(hipEventRecord(ev_chk[slot], stream));
             LDPC_HIP(hipStreamWaitEvent(stream2, ev_chk[slot], 0));
-            if ((rc = launch_var(stream2, scratch, t0, gt, pt))) return rc;
+            if ((rc = launch_var(stream2, scratch, t0, gt, pt, dev::Refill{}))) return rc;
             LDPC_HIP(hipEventRecord(ev_var[slot], stream2));
         }
         if (pipe) {  // the next syndrome needs every variable phase of this iteration
@@ -355,6 +380,7 @@ int Engine::decode(const double* d_in, int in_kind, int64_t B, int32_t max_iter,
     if (B < 0 || max_iter < 0) { set_error("B and max_iter must be >= 0"); return LDPC_ERR_ARG; }
     if (B == 0) return LDPC_OK;
     LDPC_HIP(hipSetDevice(device));
+    if (cont) return run_cont(d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
     // balanced passes of <= cap codewords (multiples of 64 except the tail)
     const int64_t npass = (B + cap - 1) / cap;
     const int64_t per = std::min<int64_t>(cap, ((B + npass - 1) / npass + 63) / 64 * 64);
@@ -365,6 +391,58 @@ int Engine::decode(const double* d_in, int in_kind, int64_t B, int32_t max_iter,
                            d_post ? d_post + (size_t)b0 * N : nullptr, post_kind, d_iters ? d_iters + b0 : nullptr,
                            d_valid ? d_valid + b0 : nullptr);
         if (rc) return rc;
+    }
+    return LDPC_OK;
+}
+
+// Continuous batching over the whole batch: lanes are refilled as codewords
+// finish (kernels.hpp k_syndrome_cont), so a 64-codeword tile never idles on
+// its slowest member.  The host enqueues steps and stops kLag steps after
+// the device reports an empty pool (occupied lanes == 0 once the claim
+// counter has passed B); the few surplus steps find no occupied lane.
+int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
+                     int post_kind, int32_t* d_iters, uint8_t* d_valid)
+{
+    using namespace dev;
+    const int msa = algo == LDPC_ALGO_MSA;
+    if (msa && in_kind == LDPC_IN_LR) { set_error("min-sum takes LLR input"); return LDPC_ERR_ARG; }
+    if (msa && post_kind == LDPC_POST_RATIO) { set_error("LDPC_POST_RATIO is BP-only"); return LDPC_ERR_ARG; }
+    if (!d_hard || !d_iters || !d_valid) { set_error("continuous mode needs hard, iters and valid outputs"); return LDPC_ERR_ARG; }
+    const int32_t M = g->M, N = g->N;
+    const int64_t tiles = std::min<int64_t>(cap_tiles, (B + 63) / 64);
+    if (d_post && !post_t) LDPC_HIP(hipMalloc((void**)&post_t, (size_t)cap * N * sizeof(double)));
+    double* pt = d_post ? post_t : nullptr;
+    LDPC_HIP(hipMemsetAsync(active, 0, (size_t)tiles * sizeof(uint64_t), stream));
+    LDPC_HIP(hipMemsetAsync(d_fresh, 0, (size_t)tiles * sizeof(uint64_t), stream));
+    LDPC_HIP(hipMemsetAsync(d_occ, 0, (size_t)tiles * sizeof(uint64_t), stream));
+    LDPC_HIP(hipMemsetAsync(d_ctr, 0, sizeof(unsigned long long), stream));
+    ContState cs{active, d_fresh, d_occ, d_lane_b, d_lane_n, d_ctr, nullptr, B};
+    ContOut co{d_hard, d_post, d_iters, d_valid, post_t, prior, msa, post_kind == LDPC_POST_RATIO ? 1 : 0};
+    const Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0};
+    const bool reg_rowT = d_col_idx_T != nullptr;
+    for (int64_t s = 0;; s++) {
+        const int slot = (int)(s % kRing);
+        cs.occ_count = d_ctr + 1 + slot;
+        LDPC_HIP(hipMemsetAsync(cs.occ_count, 0, sizeof(unsigned long long), stream));
+        if (reg_rowT)
+            LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome_cont<72>, dim3((unsigned)tiles), dim3(1024), 0, stream, hard,
+                                             d_row_ptr, d_col_idx, d_col_idx_T, M, N, max_iter, cs, co));
+        else
+            LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome_cont<0>, dim3((unsigned)tiles), dim3(1024), 0, stream, hard,
+                                             d_row_ptr, d_col_idx, d_col_idx_T, M, N, max_iter, cs, co));
+        LDPC_HIP(hipMemcpyAsync(h_occ + slot, cs.occ_count, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+        LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
+        for (int64_t t0 = 0; t0 < tiles; t0 += group_tiles) {
+            const unsigned gt = (unsigned)std::min<int64_t>(group_tiles, tiles - t0);
+            int rc;
+            if ((rc = launch_check(stream, c2v, t0, gt))) return rc;
+            if ((rc = launch_var(stream, c2v, t0, gt, pt, rf))) return rc;
+        }
+        if (s >= kLag) {
+            const int old = (int)((s - kLag) % kRing);
+            LDPC_HIP(hipEventSynchronize(ev_ring[old]));
+            if (h_occ[old] == 0) break;
+        }
     }
     return LDPC_OK;
 }

@@ -10,6 +10,7 @@
 
 #include "../../include/ldpc_amd.h"
 #include "graph.hpp"
+#include "kargs.hpp"
 
 namespace ldpc {
 
@@ -39,6 +40,15 @@ struct Engine {
     bool nt_d = false;        // nontemporal loads/stores of the v2c ("d") stream
     bool pipe = false;        // check(g+1) on `stream` overlaps variable(g) on `stream2`
     bool lr_csc = false;      // c2v scratch in column (CSC) order (regular kernels only)
+    bool cont = false;        // continuous batching: refill lanes as codewords finish
+    static constexpr int kRing = 8, kLag = 2;
+    uint64_t* d_fresh = nullptr;
+    uint64_t* d_occ = nullptr;
+    int64_t* d_lane_b = nullptr;
+    int32_t* d_lane_n = nullptr;
+    unsigned long long* d_ctr = nullptr;  // [0] claim counter, [1..kRing] occupancy ring
+    unsigned long long* h_occ = nullptr;  // pinned mirror of the occupancy ring
+    hipEvent_t ev_ring[kRing] = {};
     int32_t* d_csc_pos = nullptr;  // [E] CSC position of CSR edge e
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_chk[2] = {nullptr, nullptr}, ev_var[2] = {nullptr, nullptr}, ev_join = nullptr;
@@ -67,7 +77,9 @@ struct Engine {
 
     ~Engine();
     int init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, int64_t group = -1, int nt = -1,
-             int pipelined = -1, int csc = -1);
+             int pipelined = -1, int csc = -1, int cont_mode = -1);
+    int run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
+                 int post_kind, int32_t* d_iters, uint8_t* d_valid);
     // decode Bc <= cap codewords whose [Bc][N] input is at d_in (device)
     int run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_iter, uint8_t* d_hard, double* d_post,
                   int post_kind, int32_t* d_iters, uint8_t* d_valid);
@@ -82,7 +94,7 @@ struct Engine {
     int mark_begin(KClass c, hipStream_t s, hipEvent_t* b);
     int mark_end(KClass c, hipStream_t s, hipEvent_t b);
     int launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt);
-    int launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt);
+    int launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt, const dev::Refill& rf);
 };
 
 // bytes of device memory per resident codeword

@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "kargs.hpp"
+
 namespace ldpc {
 namespace dev {
 
@@ -274,25 +276,35 @@ __global__ __launch_bounds__(256) void k_check_bp_gen(const double* __restrict__
 // post (optional) receives P, the posterior ratio of this iteration.
 // grid (ceil(N/4), group tiles), block 256: one wave per (column, tile).
 // ---------------------------------------------------------------------------
-template <int DV, bool NT, bool CSCL>
+template <int DV, bool NT, bool CSCL, bool CONT>
 __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, double* __restrict__ dmsg,
-                                                const double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                                double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                 const uint64_t* __restrict__ active, const int32_t* __restrict__ col_edge,
-                                                double* __restrict__ post, int32_t N, int64_t E, int64_t t0)
+                                                double* __restrict__ post, int32_t N, int64_t E, int64_t t0, Refill rf)
 {
     const int lane = lane_id();
     const int32_t j = blockIdx.x * 4 + wave_id();
     const int64_t t = t0 + blockIdx.y;
     if (j >= N) return;
     const uint64_t act = active[t];
-    if (act == 0) return;
+    const uint64_t frm = CONT ? rf.fresh[t] : 0ull;
+    const uint64_t touched = act | frm;
+    if (touched == 0) return;
     const bool live = (act >> lane) & 1ull;
     int32_t eid[DV];
 #pragma unroll
     for (int s = 0; s < DV; ++s) eid[s] = col_edge[(size_t)j * DV + s];
     const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
     bool h = false;
-    if (live) {
+    if (CONT && ((frm >> lane) & 1ull)) {  // Init_Belief_Propagation for a refilled lane
+        const double x = rf.in[(size_t)rf.lane_b[t * TILE + lane] * N + j];
+        const double LR = rf.in_is_llr ? exp(x) : x;
+        prior[((size_t)t * N + j) * TILE + lane] = LR;
+        const double d0 = 1.0 - 2.0 / (1.0 + LR);
+#pragma unroll
+        for (int s = 0; s < DV; ++s) st<NT>(dmsg + (tb + eid[s]) * TILE + lane, d0);
+        h = (LR < 1.0);
+    } else if (live) {
         const size_t pj = ((size_t)t * N + j) * TILE + lane;
         const double LR = prior[pj];
         double l[DV], pr[DV];
@@ -316,8 +328,8 @@ __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, d
     const uint64_t m = __ballot(h);
     if (lane == 0) {
         const size_t o = (size_t)t * N + j;
-        const uint64_t old = (act == ~0ull) ? 0ull : hard[o];
-        hard[o] = (old & ~act) | (m & act);
+        const uint64_t old = (touched == ~0ull) ? 0ull : hard[o];
+        hard[o] = (old & ~touched) | (m & touched);
     }
 }
 
@@ -475,25 +487,33 @@ __global__ __launch_bounds__(256) void k_check_msa_gen(const double* __restrict_
 //   v2c_s = ((LLR + c_0) + c_1) ... skipping c_s, ascending row order
 //   L = LLR + c_0 + ... + c_{DV-1};  dblk = !(L > 0);  post (optional) <- L
 // ---------------------------------------------------------------------------
-template <int DV, bool NT, bool CSCL>
+template <int DV, bool NT, bool CSCL, bool CONT>
 __global__ __launch_bounds__(256) void k_var_msa(const double* __restrict__ c2v, double* __restrict__ v2c,
-                                                 const double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                                 double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                  const uint64_t* __restrict__ active, const int32_t* __restrict__ col_edge,
-                                                 double* __restrict__ post, int32_t N, int64_t E, int64_t t0)
+                                                 double* __restrict__ post, int32_t N, int64_t E, int64_t t0, Refill rf)
 {
     const int lane = lane_id();
     const int32_t j = blockIdx.x * 4 + wave_id();
     const int64_t t = t0 + blockIdx.y;
     if (j >= N) return;
     const uint64_t act = active[t];
-    if (act == 0) return;
+    const uint64_t frm = CONT ? rf.fresh[t] : 0ull;
+    const uint64_t touched = act | frm;
+    if (touched == 0) return;
     const bool live = (act >> lane) & 1ull;
     int32_t eid[DV];
 #pragma unroll
     for (int s = 0; s < DV; ++s) eid[s] = col_edge[(size_t)j * DV + s];
     const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
     bool h = false;
-    if (live) {
+    if (CONT && ((frm >> lane) & 1ull)) {  // Init_MSA_INF for a refilled lane
+        const double x = rf.in[(size_t)rf.lane_b[t * TILE + lane] * N + j];
+        prior[((size_t)t * N + j) * TILE + lane] = x;
+#pragma unroll
+        for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[s]) * TILE + lane, x);
+        h = !(x > 0);
+    } else if (live) {
         const size_t pj = ((size_t)t * N + j) * TILE + lane;
         const double llr = prior[pj];
         double c[DV];
@@ -516,8 +536,8 @@ __global__ __launch_bounds__(256) void k_var_msa(const double* __restrict__ c2v,
     const uint64_t m = __ballot(h);
     if (lane == 0) {
         const size_t o = (size_t)t * N + j;
-        const uint64_t old = (act == ~0ull) ? 0ull : hard[o];
-        hard[o] = (old & ~act) | (m & act);
+        const uint64_t old = (touched == ~0ull) ? 0ull : hard[o];
+        hard[o] = (old & ~touched) | (m & touched);
     }
 }
 
@@ -590,6 +610,110 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ pos
         out = post_ratio ? P : log(P);
     }
     post[(size_t)b * N + j] = out;
+}
+
+// ---------------------------------------------------------------------------
+// Continuous-batching syndrome step (one block per tile).  For every occupied
+// lane (a codeword after lane_n iterations, or just initialised: lane_n = 0):
+//   c == 0 or lane_n == max_iter  -> finished (Run_*_Decoder loop control,
+//       dec.cpp:594-599 / 1223-1246): iters = lane_n, valid = (c == 0), hard
+//       bits (and posterior) written to the codeword's output row; lane freed;
+//   otherwise                    -> lane_n += 1, stays active.
+// Free lanes claim the next codeword indices from a global counter (atomic)
+// and are initialised by the following variable kernel (`fresh` mask).
+// Which lane decodes which codeword varies run to run; each codeword's
+// arithmetic does not.
+// ---------------------------------------------------------------------------
+template <int DC>
+__global__ __launch_bounds__(1024) void k_syndrome_cont(const uint64_t* __restrict__ hard,
+                                                        const int32_t* __restrict__ row_ptr,
+                                                        const int32_t* __restrict__ col_idx,
+                                                        const int32_t* __restrict__ col_idx_T, int32_t M, int32_t N,
+                                                        int32_t max_iter, ContState cs, ContOut co)
+{
+    __shared__ uint64_t red[16];
+    __shared__ int64_t s_b[TILE];
+    __shared__ int32_t s_n[TILE];
+    __shared__ uint64_t s_fin;
+    const int64_t t = blockIdx.x;
+    const uint64_t occ = cs.occupied[t];
+    const int lane = lane_id(), w = wave_id();
+    const uint64_t* h = hard + (size_t)t * N;
+    uint64_t u = 0;
+    if (occ) {
+        for (int32_t i = threadIdx.x; i < M; i += blockDim.x) {
+            uint64_t p = 0;
+            if (DC > 0) {
+#pragma unroll 24
+                for (int k = 0; k < DC; ++k) p ^= h[col_idx_T[(size_t)k * M + i]];
+            } else {
+                for (int32_t e = row_ptr[i]; e < row_ptr[i + 1]; ++e) p ^= h[col_idx[e]];
+            }
+            u |= p;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) u |= shfl_xor_u64(u, off);
+        if (lane == 0) red[w] = u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint64_t U = 0;
+        if (occ)
+            for (int q = 0; q < (int)(blockDim.x >> 6); ++q) U |= red[q];
+        const size_t li = (size_t)t * TILE + lane;
+        const bool o = (occ >> lane) & 1ull;
+        const int32_t ln = o ? cs.lane_n[li] : 0;
+        const bool unsat = (U >> lane) & 1ull;
+        const bool fin = o && (!unsat || ln == max_iter);
+        const bool cont = o && !fin;
+        const int64_t b = o ? cs.lane_b[li] : -1;
+        if (fin) { co.iters[b] = ln; co.valid[b] = unsat ? 0 : 1; }
+        s_b[lane] = b;
+        s_n[lane] = ln;
+        const uint64_t F = __ballot(fin), Cm = __ballot(cont);
+        // refill every lane that is not continuing
+        const uint64_t freem = ~Cm;
+        const int nfree = __popcll(freem);
+        unsigned long long base = 0;
+        if (lane == 0) {
+            const unsigned long long nb = __hip_atomic_load(cs.next_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            base = (nb < (unsigned long long)cs.B) ? atomicAdd(cs.next_b, (unsigned long long)nfree) : nb;
+        }
+        base = __shfl(base, 0);
+        const int rank = __popcll(freem & ((1ull << lane) - 1ull));
+        const bool fresh = !cont && (base + (unsigned long long)rank < (unsigned long long)cs.B);
+        const uint64_t Fr = __ballot(fresh);
+        if (cont) cs.lane_n[li] = ln + 1;
+        if (fresh) { cs.lane_b[li] = (int64_t)(base + rank); cs.lane_n[li] = 0; }
+        if (lane == 0) {
+            cs.active[t] = Cm;
+            cs.fresh[t] = Fr;
+            cs.occupied[t] = Cm | Fr;
+            s_fin = F;
+            if (Cm | Fr) atomicAdd(cs.occ_count, (unsigned long long)__popcll(Cm | Fr));
+        }
+    }
+    __syncthreads();
+    // write the finished codewords' outputs (hard bits of this step, posterior)
+    uint64_t F = s_fin;
+    if (!F) return;
+    for (int32_t j = threadIdx.x; j < N; j += blockDim.x) {
+        const uint64_t wj = h[j];
+        for (uint64_t f = F; f; f &= f - 1) {
+            const int l = __builtin_ctzll(f);
+            const size_t ob = (size_t)s_b[l] * N + j;
+            co.hard[ob] = (uint8_t)((wj >> l) & 1ull);
+            if (co.post) {
+                const size_t pj = ((size_t)t * N + j) * TILE + l;
+                const double pv = s_n[l] > 0 ? co.post_t[pj] : co.prior[pj];
+                if (co.algo_msa) co.post[ob] = pv;
+                else {
+                    const double P = __builtin_isnan(pv) ? 1.0 : pv;
+                    co.post[ob] = co.post_ratio ? P : log(P);
+                }
+            }
+        }
+    }
 }
 
 // hard ballots -> [b][N] u8 (the reference's dblk / dec_*.txt bits)

@@ -95,7 +95,7 @@ def lib():
         L.ldpc_decode.argtypes = [vp, vp, i64, i32, i32, vp, vp, vp, vp, C.POINTER(Opts)]
         L.ldpc_engine_create.argtypes = [vp, i32, i32, i64, pint]
         L.ldpc_engine_create.restype = vp
-        L.ldpc_engine_create_ex.argtypes = [vp, i32, i32, i64, i64, i32, pint]
+        L.ldpc_engine_create_ex.argtypes = [vp, i32, i32, i64, i64, i32, i32, pint]
         L.ldpc_engine_create_ex.restype = vp
         L.ldpc_engine_info.argtypes = [vp, vp, vp, vp]
         L.ldpc_engine_free.argtypes = [vp]
@@ -359,20 +359,23 @@ class DeviceBuffer:
 class Engine:
     def __init__(self, g: Graph, device: int = 0, algo="bp", chunk: int = 0, group_tiles: int = -1,
                  nontemporal: Optional[bool] = None, pipeline: Optional[bool] = None,
-                 csc_scratch: Optional[bool] = None):
+                 csc_scratch: Optional[bool] = None, continuous: Optional[bool] = None):
         self.g, self.device, self.algo = g, device, _algo(algo)
         err = C.c_int(0)
-        if nontemporal is None and pipeline is None and csc_scratch is None:
-            flags = -1
-        else:
-            flags = int(bool(nontemporal)) | (int(bool(pipeline)) << 1) | (int(bool(csc_scratch)) << 2)
-        self._h = lib().ldpc_engine_create_ex(g.handle, device, self.algo, chunk, group_tiles, flags, C.byref(err))
+        flags_set = flags = 0
+        for bit, v in enumerate((nontemporal, pipeline, csc_scratch, continuous)):
+            if v is not None:
+                flags_set |= 1 << bit
+                flags |= int(bool(v)) << bit
+        self._h = lib().ldpc_engine_create_ex(g.handle, device, self.algo, chunk, group_tiles, flags_set, flags,
+                                              C.byref(err))
         if not self._h:
             raise LdpcError(err.value, (lib().ldpc_last_error() or b"").decode())
         cap, grp, fl = C.c_int64(), C.c_int64(), C.c_int32()
         _check(lib().ldpc_engine_info(self._h, C.byref(cap), C.byref(grp), C.byref(fl)))
         self.cap, self.group_tiles = cap.value, grp.value
         self.nontemporal, self.pipeline, self.csc_scratch = bool(fl.value & 1), bool(fl.value & 2), bool(fl.value & 4)
+        self.continuous = bool(fl.value & 8)
 
     def decode(self, d_in, in_kind: int, B: int, max_iter: int, d_hard=None, d_post=None, post_kind=POST_LLR,
                d_iters=None, d_valid=None):

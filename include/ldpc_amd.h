@@ -128,12 +128,15 @@ ldpc_engine *ldpc_engine_create(const ldpc_graph *g, int32_t device, int32_t alg
 /* Same with the schedule knobs: group_tiles = 64-codeword tiles per
  * check/variable launch (the check->variable messages of one group stay
  * resident in the Infinity Cache; 0 = whole pass, -1 = default / env
- * LDPC_GROUP_TILES); flags bit 0 = nontemporal v2c stream, bit 1 = overlap
+ * LDPC_GROUP_TILES).  Schedule flags: the bits set in flags_set are taken
+ * from flags, the others from the defaults / environment.
+ * Bit 0 = nontemporal v2c stream, bit 1 = overlap
  * check(g+1) with variable(g) on a second stream, bit 2 = check->variable
- * messages stored in column order (flags -1 = defaults / env LDPC_NT_D,
- * LDPC_PIPE, LDPC_LR_CSC). */
+ * messages stored in column order, bit 3 = continuous batching (a finished
+ * codeword's lane is refilled with the next one; needs hard/iters/valid
+ * outputs) (env LDPC_NT_D, LDPC_PIPE, LDPC_LR_CSC, LDPC_CONT). */
 ldpc_engine *ldpc_engine_create_ex(const ldpc_graph *g, int32_t device, int32_t algo, int64_t chunk,
-                                   int64_t group_tiles, int32_t flags, int *err);
+                                   int64_t group_tiles, int32_t flags_set, int32_t flags, int *err);
 void ldpc_engine_free(ldpc_engine *e);
 
 /* Decode B codewords whose input already lives in device memory (d_in:

@@ -209,9 +209,10 @@ def test_multi_device_api_single_gpu_box(G, og, codewords):
     _cmp(G, og, llr, 20, devices=[0, 0])
 
 
-@pytest.mark.parametrize("group,nt,pipe,csc", [(1, 0, 0, 0), (1, 1, 1, 1), (3, 0, 1, 0), (2, 1, 0, 1), (0, 1, 0, 0),
-                                                (0, 0, 0, 1)])
-def test_grouped_schedules_bitexact(gpu, og, codewords, monkeypatch, group, nt, pipe, csc):
+@pytest.mark.parametrize("group,nt,pipe,csc,cont", [(1, 0, 0, 0, 0), (1, 1, 1, 1, 0), (3, 0, 1, 0, 0), (2, 1, 0, 1, 0),
+                                                     (0, 1, 0, 0, 0), (0, 0, 0, 1, 0), (3, 1, 0, 0, 1), (1, 0, 0, 1, 1),
+                                                     (0, 1, 0, 0, 1)])
+def test_grouped_schedules_bitexact(gpu, og, codewords, monkeypatch, group, nt, pipe, csc, cont):
     """The Infinity-Cache-resident schedule (check->variable messages of one
     tile group at a time) and the nontemporal d-stream change only the launch
     order across codewords, never a codeword's arithmetic."""
@@ -219,8 +220,23 @@ def test_grouped_schedules_bitexact(gpu, og, codewords, monkeypatch, group, nt, 
     monkeypatch.setenv("LDPC_NT_D", str(nt))
     monkeypatch.setenv("LDPC_PIPE", str(pipe))
     monkeypatch.setenv("LDPC_LR_CSC", str(csc))
+    monkeypatch.setenv("LDPC_CONT", str(cont))
     G2 = gpu.Graph(PCHK)  # fresh graph -> fresh engine pool reads the env
     llr = synth.dna_like_llrs(codewords, seed=1, reads=57000)[:200]
     _cmp(G2, og, llr, 60)
     llr = synth.bsc_llrs(codewords, 0, 200, seed=2026, p=0.002)
     _cmp(G2, og, llr, 30, algo="msa")
+
+
+@pytest.mark.parametrize("chunk", [64, 128])
+def test_continuous_batching_edge_cases(gpu, og, codewords, monkeypatch, chunk):
+    """Continuous mode with a pool smaller than the batch (lanes are refilled
+    many times), mixed early exits, max_iter 0, B not a multiple of 64, and
+    the posterior written at each codeword's own exit."""
+    monkeypatch.setenv("LDPC_CONT", "1")
+    G2 = gpu.Graph(PCHK)
+    llr = np.concatenate([synth.bsc_llrs(codewords, 0, 150, seed=3, p=0.003),
+                          synth.bsc_llrs(codewords, 150, 50, seed=3, p=0.02)])
+    _cmp(G2, og, llr, 25, chunk=chunk)
+    _cmp(G2, og, llr[:70], 0, chunk=chunk)
+    _cmp(G2, og, llr[:130], 12, algo="msa", chunk=chunk)
