@@ -156,7 +156,9 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     lr_csc = csc != 0 && g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
     const size_t E = (size_t)std::max<int64_t>(g->E, 1);
     LDPC_HIP(hipMalloc((void**)&v2c, (size_t)cap * E * sizeof(double)));
-    LDPC_HIP(hipMalloc((void**)&c2v, (size_t)(pipe ? 2 : 1) * group_tiles * 64 * E * sizeof(double)));
+    // continuous mode's drain tail (< 1/32 occupancy) launches wider groups
+    c2v_tiles = std::max<int64_t>((pipe ? 2 : 1) * group_tiles, cont ? (cap_tiles + 3) / 4 : 0);
+    LDPC_HIP(hipMalloc((void**)&c2v, (size_t)c2v_tiles * 64 * E * sizeof(double)));
     LDPC_HIP(hipMalloc((void**)&prior, (size_t)cap * g->N * sizeof(double)));
     LDPC_HIP(hipMalloc((void**)&hard, (size_t)cap_tiles * g->N * sizeof(uint64_t)));
     LDPC_HIP(hipMalloc((void**)&active, (size_t)cap_tiles * sizeof(uint64_t)));
@@ -420,6 +422,11 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     ContOut co{d_hard, d_post, d_iters, d_valid, post_t, prior, msa, post_kind == LDPC_POST_RATIO ? 1 : 0};
     const Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0};
     const bool reg_rowT = d_col_idx_T != nullptr;
+    // While the pool is mostly occupied, launch per tile group (c2v stays in the
+    // Infinity Cache); once the input is drained and few lanes remain, one
+    // check + one variable launch over all tiles per step (the tail is launch-
+    // bound, and the c2v traffic is small).  `low` lags the device by kLag.
+    bool low = false;
     for (int64_t s = 0;; s++) {
         const int slot = (int)(s % kRing);
         cs.occ_count = d_ctr + 1 + slot;
@@ -432,8 +439,9 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                                              d_row_ptr, d_col_idx, d_col_idx_T, M, N, max_iter, cs, co));
         LDPC_HIP(hipMemcpyAsync(h_occ + slot, cs.occ_count, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
         LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
-        for (int64_t t0 = 0; t0 < tiles; t0 += group_tiles) {
-            const unsigned gt = (unsigned)std::min<int64_t>(group_tiles, tiles - t0);
+        const int64_t gstep = low ? std::max(group_tiles, c2v_tiles) : group_tiles;
+        for (int64_t t0 = 0; t0 < tiles; t0 += gstep) {
+            const unsigned gt = (unsigned)std::min<int64_t>(gstep, tiles - t0);
             int rc;
             if ((rc = launch_check(stream, c2v, t0, gt))) return rc;
             if ((rc = launch_var(stream, c2v, t0, gt, pt, rf))) return rc;
@@ -442,6 +450,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             const int old = (int)((s - kLag) % kRing);
             LDPC_HIP(hipEventSynchronize(ev_ring[old]));
             if (h_occ[old] == 0) break;
+            low = h_occ[old] * 32 < (unsigned long long)(tiles * 64);
         }
     }
     return LDPC_OK;

@@ -37,6 +37,7 @@ struct Engine {
     int64_t cap = 0;        // codewords per pass (multiple of 64)
     int64_t cap_tiles = 0;
     int64_t group_tiles = 0;  // tiles per check/variable launch; c2v holds only one group
+    int64_t c2v_tiles = 0;    // tiles of c2v scratch allocated
     bool nt_d = false;        // nontemporal loads/stores of the v2c ("d") stream
     bool pipe = false;        // check(g+1) on `stream` overlaps variable(g) on `stream2`
     bool lr_csc = false;      // c2v scratch in column (CSC) order (regular kernels only)

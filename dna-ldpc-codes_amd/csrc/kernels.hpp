@@ -32,6 +32,17 @@ constexpr int TILE = 64;
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// XCD-aware block order (cdna_hip_programming.md T1): blocks b and b+8 share an
+// XCD under round-robin dispatch, so give each b % 8 group a contiguous range
+// of logical blocks (bijective for any grid size).  Speed only, never
+// correctness: neighbouring column groups then share the XCD's L2 (refill
+// input rows, hard-bit words).
+__device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned nb)
+{
+    const unsigned q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m)
 {
     uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
@@ -283,7 +294,7 @@ __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, d
                                                 double* __restrict__ post, int32_t N, int64_t E, int64_t t0, Refill rf)
 {
     const int lane = lane_id();
-    const int32_t j = blockIdx.x * 4 + wave_id();
+    const int32_t j = xcd_block(blockIdx.x, gridDim.x) * 4 + wave_id();
     const int64_t t = t0 + blockIdx.y;
     if (j >= N) return;
     const uint64_t act = active[t];
@@ -296,16 +307,18 @@ __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, d
     for (int s = 0; s < DV; ++s) eid[s] = col_edge[(size_t)j * DV + s];
     const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
     bool h = false;
-    if (CONT && ((frm >> lane) & 1ull)) {  // Init_Belief_Propagation for a refilled lane
+    const bool fr = CONT && ((frm >> lane) & 1ull);
+    double dv[DV];  // the d values this lane stores (update or initial)
+    const size_t pj = ((size_t)t * N + j) * TILE + lane;
+    if (fr) {  // Init_Belief_Propagation for a refilled lane
         const double x = rf.in[(size_t)rf.lane_b[t * TILE + lane] * N + j];
         const double LR = rf.in_is_llr ? exp(x) : x;
-        prior[((size_t)t * N + j) * TILE + lane] = LR;
+        prior[pj] = LR;
         const double d0 = 1.0 - 2.0 / (1.0 + LR);
 #pragma unroll
-        for (int s = 0; s < DV; ++s) st<NT>(dmsg + (tb + eid[s]) * TILE + lane, d0);
+        for (int s = 0; s < DV; ++s) dv[s] = d0;
         h = (LR < 1.0);
     } else if (live) {
-        const size_t pj = ((size_t)t * N + j) * TILE + lane;
         const double LR = prior[pj];
         double l[DV], pr[DV];
 #pragma unroll
@@ -322,8 +335,12 @@ __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, d
             double v = pr[s] * acc;
             if (__builtin_isnan(v)) v = 1.0;
             acc = acc * l[s];
-            st<NT>(dmsg + (tb + eid[s]) * TILE + lane, 1.0 - 2.0 / (1.0 + v));
+            dv[s] = 1.0 - 2.0 / (1.0 + v);
         }
+    }
+    if (fr || live) {  // one store sequence for both kinds of lane
+#pragma unroll
+        for (int s = 0; s < DV; ++s) st<NT>(dmsg + (tb + eid[s]) * TILE + lane, dv[s]);
     }
     const uint64_t m = __ballot(h);
     if (lane == 0) {
@@ -494,7 +511,7 @@ __global__ __launch_bounds__(256) void k_var_msa(const double* __restrict__ c2v,
                                                  double* __restrict__ post, int32_t N, int64_t E, int64_t t0, Refill rf)
 {
     const int lane = lane_id();
-    const int32_t j = blockIdx.x * 4 + wave_id();
+    const int32_t j = xcd_block(blockIdx.x, gridDim.x) * 4 + wave_id();
     const int64_t t = t0 + blockIdx.y;
     if (j >= N) return;
     const uint64_t act = active[t];
@@ -507,14 +524,16 @@ __global__ __launch_bounds__(256) void k_var_msa(const double* __restrict__ c2v,
     for (int s = 0; s < DV; ++s) eid[s] = col_edge[(size_t)j * DV + s];
     const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
     bool h = false;
-    if (CONT && ((frm >> lane) & 1ull)) {  // Init_MSA_INF for a refilled lane
+    const bool fr = CONT && ((frm >> lane) & 1ull);
+    double dv[DV];  // the v2c values this lane stores (update or initial)
+    const size_t pj = ((size_t)t * N + j) * TILE + lane;
+    if (fr) {  // Init_MSA_INF for a refilled lane
         const double x = rf.in[(size_t)rf.lane_b[t * TILE + lane] * N + j];
-        prior[((size_t)t * N + j) * TILE + lane] = x;
+        prior[pj] = x;
 #pragma unroll
-        for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[s]) * TILE + lane, x);
+        for (int s = 0; s < DV; ++s) dv[s] = x;
         h = !(x > 0);
     } else if (live) {
-        const size_t pj = ((size_t)t * N + j) * TILE + lane;
         const double llr = prior[pj];
         double c[DV];
 #pragma unroll
@@ -525,13 +544,17 @@ __global__ __launch_bounds__(256) void k_var_msa(const double* __restrict__ c2v,
 #pragma unroll
             for (int r = 0; r < DV; ++r)
                 if (r != s) sum = sum + c[r];
-            st<NT>(v2c + (tb + eid[s]) * TILE + lane, sum);
+            dv[s] = sum;
         }
         double L = llr;
 #pragma unroll
         for (int s = 0; s < DV; ++s) L = L + c[s];
         h = !(L > 0);
         if (post) post[pj] = L;
+    }
+    if (fr || live) {  // one store sequence for both kinds of lane
+#pragma unroll
+        for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[s]) * TILE + lane, dv[s]);
     }
     const uint64_t m = __ballot(h);
     if (lane == 0) {
