@@ -170,7 +170,9 @@ def main():
     G = L.Graph(synth.PCHK)
     N, E = G.N, G.E
     B = args.batch_per_gpu
-    dev = local
+    # one GPU per local rank; ranks share devices round-robin when there are
+    # fewer GPUs than ranks (rehearsals on a one-GPU box)
+    dev = local % max(1, L.device_count())
     algo = args.algo
     eng = L.Engine(G, dev, algo, chunk=args.chunk, group_tiles=args.group_tiles,
                    nontemporal=None if args.nt < 0 else bool(args.nt), pipeline=None if args.pipe < 0 else bool(args.pipe),

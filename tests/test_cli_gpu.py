@@ -1,0 +1,74 @@
+"""The file-compatible ldpc CLI and ldpc_amd.decode_files on the GPU (the
+ldpc.exe contract, DNA_main.cpp:300-505, 916-927, 965-1182)."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import synth
+from conftest import PCHK, ROOT
+
+pytestmark = pytest.mark.gpu
+EXE = os.path.join(ROOT, "dna-ldpc-codes_amd", "bin", "ldpc")
+
+
+def _write_inputs(d, codeword, llr, i=1):
+    cwb = f"codeword_n18432_m1860_{i}"
+    soft = f"soft72000_n18432_m1860_{i}"
+    with open(os.path.join(d, cwb + ".txt"), "w") as f:  # def_func.write_codeword format
+        f.write("".join(f"{int(b)} " for b in codeword))
+    with open(os.path.join(d, soft + ".txt"), "w") as f:  # str(float) as decoder.py:533
+        f.write("".join(str(float(v)) + " " for v in llr))
+    shutil.copyfile(PCHK, os.path.join(d, "decode_n18432_m2048_final.pchk"))
+    return cwb, soft
+
+
+@pytest.mark.parametrize("algo,dtype", [("bp", 0), ("msa", 20)])
+def test_cli_matches_oracle(tmp_path, og, codewords, algo, dtype):
+    d = str(tmp_path)
+    llr = synth.dna_like_llrs(codewords, seed=1, reads=57000)[13]  # codeword 14: a BP failure case
+    if algo == "msa":
+        llr = synth.bsc_llrs(codewords, 0, 1, seed=2026, p=0.002)[0]
+    cwb, soft = _write_inputs(d, codewords[13] if algo == "bp" else codewords[0], llr)
+    argv = [EXE, "0", str(dtype), "0", "7", "200", "1", cwb, soft, "decode_n18432_m2048_final", "0", "0", "0", "0"]
+    r = subprocess.run(argv, cwd=d, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "g_CODE_N : 18432" in r.stdout and f"dec_{cwb}.txt" in r.stdout
+    dec = np.array(open(os.path.join(d, f"dec_{cwb}.txt")).read().split(), dtype=np.uint8)
+    h, _, it, v = og.decode_batch(llr[None, :], 200, algo=0 if algo == "bp" else 1, threads=1, want_post=False)
+    assert np.array_equal(dec, h[0])
+    res = os.path.join(d, f"result_({soft}.txt)_decode_n18432_m2048_final.pchk_{dtype}_0.000dB_0_200_7.txt")
+    txt = open(res).read()
+    assert "dv            : 8" in txt and "dc            : 72" in txt and "bRegular_dc   : 1" in txt
+    truth = codewords[13] if algo == "bp" else codewords[0]
+    nerr = int((h[0] != truth).sum())
+    assert f"# of Bit Errors[ 1]     : {nerr}" in txt
+    raw = int((truth != (llr < 0)).sum())
+    assert f"# of Bit Errors[ 0]     : {raw}" in txt
+
+
+def test_decode_files_matches_cli(tmp_path, codewords, gpu):
+    d = str(tmp_path)
+    llr = synth.dna_like_llrs(codewords, seed=0)[4]
+    cwb, soft = _write_inputs(d, codewords[4], llr, i=5)
+    out = gpu.decode_files(cwb, soft, "decode_n18432_m2048_final", max_iter=200, directory=d)
+    assert out["bit_errors"] == 0 and out["valid"]
+    py_dec = open(os.path.join(d, out["dec_file"])).read()
+    os.remove(os.path.join(d, out["dec_file"]))
+    subprocess.run([EXE, "0", "0", "0", "7", "200", "1", cwb, soft, "decode_n18432_m2048_final", "0", "0", "0", "0"],
+                   cwd=d, check=True, capture_output=True, timeout=120)
+    assert open(os.path.join(d, out["dec_file"])).read() == py_dec
+
+
+def test_cli_targeting_and_frames(tmp_path, codewords):
+    d = str(tmp_path)
+    llr = synth.bsc_llrs(codewords, 0, 1, seed=1, p=0.02)[0]
+    cwb, soft = _write_inputs(d, codewords[0], llr)
+    argv = [EXE, "0", "0", "0", "7", "5", "3", cwb, soft, "decode_n18432_m2048_final", "0", "0", "0", "1", "1", "100"]
+    r = subprocess.run(argv, cwd=d, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    res = os.path.join(d, f"result_({soft}.txt)_decode_n18432_m2048_final.pchk_0_0.000dB_0_5_7.txt")
+    txt = open(res).read()
+    assert "target_VN:1~100" in txt and "# of Frame[ 0]          :3" in txt
