@@ -161,6 +161,49 @@ ldpc_graph* ldpc_graph_from_edges(int32_t M, int32_t N, const int32_t* rows, con
     return g.release();
 }
 
+ldpc_graph* ldpc_graph_load_alist(const char* alist_path, int32_t transpose, int* err)
+{
+    if (!alist_path) { set_error("null path"); fail(LDPC_ERR_ARG, err); return nullptr; }
+    auto g = std::make_unique<ldpc_graph>();
+    std::string msg;
+    int rc = ldpc::load_alist(alist_path, transpose != 0, g->h, &msg);
+    if (rc) { set_error(msg); fail(rc, err); return nullptr; }
+    if (err) *err = LDPC_OK;
+    return g.release();
+}
+
+ldpc_graph* ldpc_graph_rs_ldpc(int32_t s, int32_t rho, int32_t gamma, int32_t* gen_poly, int32_t* coset,
+                              int* err)
+{
+    auto g = std::make_unique<ldpc_graph>();
+    std::string msg;
+    std::vector<int> gp, cs;
+    int rc = ldpc::build_rs_ldpc(s, rho, gamma, g->h, &gp, &cs, &msg);
+    if (rc) { set_error(msg); fail(rc, err); return nullptr; }
+    if (gen_poly) std::copy(gp.begin(), gp.end(), gen_poly);
+    if (coset) std::copy(cs.begin(), cs.end(), coset);
+    if (err) *err = LDPC_OK;
+    return g.release();
+}
+
+int ldpc_graph_save_pchk(const ldpc_graph* g, const char* pchk_path)
+{
+    if (!g || !pchk_path) { set_error("null argument"); return LDPC_ERR_ARG; }
+    std::string msg;
+    int rc = ldpc::save_pchk(g->h, pchk_path, &msg);
+    if (rc) set_error(msg);
+    return rc;
+}
+
+int ldpc_graph_save_alist(const ldpc_graph* g, const char* alist_path)
+{
+    if (!g || !alist_path) { set_error("null argument"); return LDPC_ERR_ARG; }
+    std::string msg;
+    int rc = ldpc::save_alist(g->h, alist_path, &msg);
+    if (rc) set_error(msg);
+    return rc;
+}
+
 void ldpc_graph_free(ldpc_graph* g) { delete g; }
 
 int ldpc_graph_info(const ldpc_graph* g, int32_t* M, int32_t* N, int64_t* E, int32_t* dv_max, int32_t* regular_dv,

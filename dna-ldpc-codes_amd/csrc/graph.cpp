@@ -14,8 +14,10 @@
 #include "graph.hpp"
 
 #include <algorithm>
+#include <cctype>
 #include <cstdio>
 #include <cstring>
+#include <set>
 
 #include "../../include/ldpc_amd.h"
 
@@ -150,6 +152,314 @@ int syndrome_host(const HostGraph& g, const uint8_t* dblk, uint8_t* pchk)
         c += p;
     }
     return c;
+}
+
+// ---------------------------------------------------------------------------
+// alist / pchk writers and the alist reader
+// ---------------------------------------------------------------------------
+
+namespace {
+
+// fscanf("%d") on a whitespace-separated stream: 1 = got a value, 0 = a
+// non-numeric token (not EOF), -1 = end of input.
+struct IntScanner {
+    std::vector<char> buf;
+    size_t pos = 0;
+    int next(int* v)
+    {
+        while (pos < buf.size() && std::isspace((unsigned char)buf[pos])) pos++;
+        if (pos >= buf.size()) return -1;
+        size_t p = pos;
+        if (buf[p] == '+' || buf[p] == '-') p++;
+        if (p >= buf.size() || !std::isdigit((unsigned char)buf[p])) return 0;
+        long long x = 0;
+        const bool neg = buf[pos] == '-';
+        while (p < buf.size() && std::isdigit((unsigned char)buf[p])) {
+            x = x * 10 + (buf[p] - '0');
+            if (x > 0x7fffffffLL) x = 0x7fffffffLL;
+            p++;
+        }
+        pos = p;
+        *v = (int)(neg ? -x : x);
+        return 1;
+    }
+};
+
+bool write_le32(FILE* f, int32_t v)
+{
+    const uint32_t u = (uint32_t)v;
+    const unsigned char b[4] = {(unsigned char)(u & 0xff), (unsigned char)((u >> 8) & 0xff),
+                                (unsigned char)((u >> 16) & 0xff), (unsigned char)((u >> 24) & 0xff)};
+    return std::fwrite(b, 1, 4, f) == 4;
+}
+
+}  // namespace
+
+int load_alist(const std::string& path, bool transpose, HostGraph& g, std::string* msg)
+{
+    FILE* f = std::fopen(path.c_str(), "r");
+    if (!f) {
+        if (msg) *msg = "Can't open alist file: " + path;  // alist-to-pchk.cpp:72-76
+        return LDPC_ERR_IO;
+    }
+    IntScanner sc;
+    char tmp[1 << 16];
+    size_t got;
+    while ((got = std::fread(tmp, 1, sizeof tmp, f)) > 0) sc.buf.insert(sc.buf.end(), tmp, tmp + got);
+    std::fclose(f);
+    auto bad = [&]() {
+        if (msg) *msg = "Alist file doesn't have the right format";  // bad_alist_file :164-168
+        return LDPC_ERR_FORMAT;
+    };
+    int M, N, mxrw, mxcw;
+    if (sc.next(&M) != 1 || M < 1 || sc.next(&N) != 1 || N < 1 || sc.next(&mxrw) != 1 || mxrw < 0 || mxrw > N ||
+        sc.next(&mxcw) != 1 || mxcw < 0 || mxcw > M)
+        return bad();
+    std::vector<int> rw((size_t)M), cw((size_t)N);
+    for (int i = 0; i < M; i++)
+        if (sc.next(&rw[(size_t)i]) != 1 || rw[(size_t)i] < 0 || rw[(size_t)i] > N) return bad();
+    for (int j = 0; j < N; j++)
+        if (sc.next(&cw[(size_t)j]) != 1 || cw[(size_t)j] < 0 || cw[(size_t)j] > M) return bad();
+    std::set<std::pair<int, int>> ent;
+    std::vector<int32_t> rows, cols;
+    long long tot = 0;
+    for (int i = 0; i < M; i++) {
+        for (int k = 0; k < mxrw; k++) {
+            int j;
+            if (sc.next(&j) != 1 || j < 0 || j > N || (k >= rw[(size_t)i] && j != 0) || (k < rw[(size_t)i] && j == 0))
+                return bad();
+            if (j == 0) continue;
+            if (!ent.insert({i, j - 1}).second) return bad();  // duplicate (mod2sparse_find)
+            rows.push_back(i);
+            cols.push_back(j - 1);
+            tot++;
+        }
+    }
+    for (int j = 0; j < N; j++) {
+        for (int k = 0; k < mxcw; k++) {
+            int i;
+            if (sc.next(&i) != 1 || i < 0 || i > M || (k >= cw[(size_t)j] && i != 0) || (k < cw[(size_t)j] && i == 0))
+                return bad();
+            if (i == 0) continue;
+            if (!ent.count({i - 1, j})) return bad();
+            tot--;
+        }
+    }
+    if (tot != 0) return bad();
+    int extra;
+    if (sc.next(&extra) != -1) return bad();  // more numbers, or trailing garbage
+    if (transpose) return build_graph(N, M, cols.data(), rows.data(), (int64_t)rows.size(), g, msg);
+    return build_graph(M, N, rows.data(), cols.data(), (int64_t)rows.size(), g, msg);
+}
+
+int save_pchk(const HostGraph& g, const std::string& path, std::string* msg)
+{
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) {
+        if (msg) *msg = "Can't create parity check file: " + path;
+        return LDPC_ERR_IO;
+    }
+    bool ok = write_le32(f, ('P' << 8) + 0x80) && write_le32(f, g.M) && write_le32(f, g.N);
+    for (int32_t i = 0; ok && i < g.M; i++) {
+        const int32_t a = g.row_ptr[(size_t)i], b = g.row_ptr[(size_t)i + 1];
+        if (a == b) continue;  // empty rows are not written (mod2sparse.cpp:357-359)
+        ok = write_le32(f, -(i + 1));
+        for (int32_t e = a; ok && e < b; e++) ok = write_le32(f, g.col_idx[(size_t)e] + 1);
+    }
+    ok = ok && write_le32(f, 0);
+    if (std::fclose(f) != 0) ok = false;
+    if (!ok) {
+        if (msg) *msg = "Error writing to parity check file " + path;
+        return LDPC_ERR_IO;
+    }
+    return LDPC_OK;
+}
+
+int save_alist(const HostGraph& g, const std::string& path, std::string* msg)
+{
+    // Layout of the alist files RS_LDPC.c:434-474 writes (every number
+    // followed by a space, one line per list), zero-padded to the maximum
+    // degree for irregular graphs as alist-to-pchk.cpp:104-124 expects.
+    FILE* f = std::fopen(path.c_str(), "w");
+    if (!f) {
+        if (msg) *msg = "Can't create alist file: " + path;
+        return LDPC_ERR_IO;
+    }
+    const int mxrw = std::max(0, g.dc_max), mxcw = std::max(0, g.dv_max);
+    std::fprintf(f, "%d %d\n%d %d\n", g.M, g.N, mxrw, mxcw);
+    for (int32_t i = 0; i < g.M; i++) std::fprintf(f, "%d ", g.row_ptr[(size_t)i + 1] - g.row_ptr[(size_t)i]);
+    std::fprintf(f, "\n");
+    for (int32_t j = 0; j < g.N; j++) std::fprintf(f, "%d ", g.col_ptr[(size_t)j + 1] - g.col_ptr[(size_t)j]);
+    std::fprintf(f, "\n");
+    for (int32_t i = 0; i < g.M; i++) {
+        int k = 0;
+        for (int32_t e = g.row_ptr[(size_t)i]; e < g.row_ptr[(size_t)i + 1]; e++, k++)
+            std::fprintf(f, "%d ", g.col_idx[(size_t)e] + 1);
+        for (; k < mxrw; k++) std::fprintf(f, "0 ");
+        std::fprintf(f, "\n");
+    }
+    for (int32_t j = 0; j < g.N; j++) {
+        int k = 0;
+        for (int32_t q = g.col_ptr[(size_t)j]; q < g.col_ptr[(size_t)j + 1]; q++, k++)
+            std::fprintf(f, "%d ", g.edge_row[(size_t)g.col_edge[(size_t)q]] + 1);
+        for (; k < mxcw; k++) std::fprintf(f, "0 ");
+        std::fprintf(f, "\n");
+    }
+    if (std::fclose(f) != 0) {
+        if (msg) *msg = "Error writing alist file " + path;
+        return LDPC_ERR_IO;
+    }
+    return LDPC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// RS-based LDPC construction (RS_LDPC.c)
+// ---------------------------------------------------------------------------
+//
+// GF(2^s) elements are carried as exponents (alpha^k, -1 = zero) exactly as
+// in the reference; addition goes through an antilog/log table pair instead
+// of its linear search over gf_table (RS_LDPC.c:119-160), which yields the
+// same exponent because the primitive polynomials make alpha^0..alpha^(q-2)
+// distinct.  Codewords are generated on the fly, and the reference's search
+// for "the first codeword equal to this coset row" (RS_LDPC.c:334-347,
+// 368-382) is an O(rho) solve: codeword index (a+1)*q + (b+1) has
+// a = cw[0] / g1[0] and b = cw[rho-1] / g2[rho-1], then a full compare.
+
+namespace {
+
+struct RsField {
+    int s = 0, q = 0, level = 0;
+    std::vector<int> tab, log;  // tab[k] = bit vector of alpha^k; log[vec] = k
+
+    bool init(int s_)
+    {
+        // RS_LDPC.c:14-93 polynominal(): low-order coefficients p0..p(s-1)
+        static const unsigned poly[11] = {0, 0, 0x3, 0x3, 0x3, 0x5, 0x3, 0x9, 0x1d, 0x11, 0x9};
+        if (s_ < 2 || s_ > 10) return false;
+        s = s_;
+        q = 1 << s;
+        level = q - 1;
+        tab.assign((size_t)level, 0);
+        log.assign((size_t)q, -1);
+        tab[0] = 1;  // RS_LDPC.c:95-117 make_table()
+        for (int i = 1; i < level; i++) {
+            int v = (tab[(size_t)i - 1] << 1) & (q - 1);
+            if (tab[(size_t)i - 1] & (1 << (s - 1))) v ^= (int)poly[s];
+            tab[(size_t)i] = v;
+        }
+        for (int i = 0; i < level; i++) {
+            if (log[(size_t)tab[(size_t)i]] != -1) return false;
+            log[(size_t)tab[(size_t)i]] = i;
+        }
+        return true;
+    }
+    int add(int i, int j) const  // gf_add, RS_LDPC.c:119-160 (C % semantics)
+    {
+        if (i == -1) return j % level;
+        if (j == -1) return i % level;
+        i %= level;
+        j %= level;
+        if (i == j) return -1;
+        return log[(size_t)(tab[(size_t)i] ^ tab[(size_t)j])];
+    }
+    int mult(int i, int j) const { return (i == -1 || j == -1) ? -1 : (i + j) % level; }  // :162-174
+    int div(int a, int b) const { return ((a - b) % level + level) % level; }  // alpha^a / alpha^b
+};
+
+}  // namespace
+
+int build_rs_ldpc(int s, int rho, int gamma, HostGraph& g, std::vector<int>* gen_poly_out,
+                  std::vector<int>* coset_out, std::string* msg)
+{
+    auto arg = [&](const char* m) {
+        if (msg) *msg = m;
+        return LDPC_ERR_ARG;
+    };
+    RsField F;
+    if (!F.init(s)) return arg("RS-LDPC: s must be in 2..10 (RS_LDPC.c:14-93 polynomial table)");
+    const int q = F.q;
+    if (rho < 3 || rho > q) return arg("RS-LDPC: rho must be in 3..2^s");
+    if (gamma < 1 || gamma > q) return arg("RS-LDPC: gamma must be in 1..2^s");
+
+    // generator polynomial (x+alpha)(x+alpha^2)... (RS_LDPC.c:176-200)
+    std::vector<int> gp((size_t)rho, 0);  // one spare slot: poly[n+1] is written at n = rho-3
+    gp[0] = 1;
+    gp[1] = 0;
+    for (int i = 1; i < rho - 2; i++) {
+        const int b = 1 + i, n = i;
+        gp[(size_t)n + 1] = gp[(size_t)n];
+        for (int k = n; k > 0; k--) gp[(size_t)k] = F.add(gp[(size_t)k - 1], F.mult(b, gp[(size_t)k]));
+        gp[0] = F.mult(b, gp[0]);
+    }
+    gp.resize((size_t)rho - 1);
+    std::vector<int> g1((size_t)rho, 0), g2((size_t)rho, 0);  // RS_LDPC.c:316-324
+    for (int i = 0; i < rho - 1; i++) {
+        g1[(size_t)i] = gp[(size_t)i];
+        g2[(size_t)i + 1] = gp[(size_t)i];
+    }
+    g1[(size_t)rho - 1] = -1;
+    g2[0] = -1;
+    if (g1[0] == -1 || g2[(size_t)rho - 1] == -1) return arg("RS-LDPC: degenerate generator polynomial");
+
+    auto codeword = [&](int idx, int* out) {  // encode(), RS_LDPC.c:202-217
+        const int a = idx / q - 1, b = idx % q - 1;
+        for (int k = 0; k < rho; k++) out[k] = F.add(F.mult(a, g1[(size_t)k]), F.mult(b, g2[(size_t)k]));
+    };
+    std::vector<int> tmp((size_t)rho);
+    auto find = [&](const int* v) -> int {  // index of the codeword equal to v, or -1
+        const int a = v[0] == -1 ? -1 : F.div(v[0], g1[0]);
+        const int b = v[rho - 1] == -1 ? -1 : F.div(v[rho - 1], g2[(size_t)rho - 1]);
+        const int idx = (a + 1) * q + (b + 1);
+        codeword(idx, tmp.data());
+        for (int k = 0; k < rho; k++)
+            if (tmp[(size_t)k] != v[k]) return -1;
+        return idx;
+    };
+
+    const int64_t ncw = (int64_t)q * q;
+    int selected = -1;
+    std::vector<int> cw((size_t)rho);
+    for (int64_t i = 0; i < ncw && selected < 0; i++) {  // RS_LDPC.c:311-329
+        codeword((int)i, cw.data());
+        int cnt = 0;
+        for (int k = 0; k < rho; k++) cnt += cw[(size_t)k] != -1;
+        if (cnt == rho) selected = (int)i;
+    }
+    if (selected < 0) return arg("RS-LDPC: no codeword of full weight rho");
+    std::vector<int> coset((size_t)ncw, -1);
+    std::vector<int> Cb((size_t)gamma * q * rho);
+    codeword(selected, cw.data());
+    for (int i = 0; i < q; i++)  // RS_LDPC.c:331-336
+        for (int k = 0; k < rho; k++) Cb[(size_t)i * rho + k] = F.mult(i - 1, cw[(size_t)k]);
+    for (int i = 0; i < q; i++) {
+        const int idx = find(&Cb[(size_t)i * rho]);
+        if (idx >= 0) coset[(size_t)idx] = 0;
+    }
+    for (int c = 1; c < gamma; c++) {  // RS_LDPC.c:352-385
+        selected = -1;
+        for (int64_t j = 0; j < ncw; j++)
+            if (coset[(size_t)j] == -1) { selected = (int)j; break; }
+        if (selected < 0) return arg("RS-LDPC: ran out of cosets");
+        codeword(selected, cw.data());
+        for (int j = 0; j < q; j++)
+            for (int k = 0; k < rho; k++)
+                Cb[((size_t)j + (size_t)c * q) * rho + k] = F.add(Cb[(size_t)j * rho + k], cw[(size_t)k]);
+        for (int j = 0; j < q; j++) {
+            const int idx = find(&Cb[((size_t)j + (size_t)c * q) * rho]);
+            if (idx >= 0) coset[(size_t)idx] = c;
+        }
+    }
+    // H[i][j*q + Cb[i][j] + 1] = 1 (RS_LDPC.c:389-398)
+    const int M = gamma * q, N = rho * q;
+    std::vector<int32_t> rows((size_t)M * rho), cols((size_t)M * rho);
+    for (int i = 0; i < M; i++)
+        for (int k = 0; k < rho; k++) {
+            rows[(size_t)i * rho + k] = i;
+            cols[(size_t)i * rho + k] = k * q + Cb[(size_t)i * rho + k] + 1;
+        }
+    if (gen_poly_out) *gen_poly_out = gp;
+    if (coset_out) *coset_out = std::move(coset);
+    return build_graph(M, N, rows.data(), cols.data(), (int64_t)rows.size(), g, msg);
 }
 
 }  // namespace ldpc

@@ -34,4 +34,22 @@ int build_graph(int32_t M, int32_t N, const int32_t* rows, const int32_t* cols, 
 // check.cpp:28-45 on the host.
 int syndrome_host(const HostGraph& g, const uint8_t* dblk, uint8_t* pchk);
 
+// alist -> graph with the validation rules of alist-to-pchk.cpp:36-160
+// (transpose = its -t option).
+int load_alist(const std::string& path, bool transpose, HostGraph& g, std::string* msg);
+
+// graph -> .pchk: magic, then mod2sparse_write (mod2sparse.cpp:338-376):
+// M, N, for every non-empty row -(i+1) and its columns+1, terminator 0.
+int save_pchk(const HostGraph& g, const std::string& path, std::string* msg);
+
+// graph -> alist (the format alist-to-pchk reads; rows then columns, 1-based,
+// zero-padded to the maximum degree).
+int save_alist(const HostGraph& g, const std::string& path, std::string* msg);
+
+// RS-based LDPC code of RS_LDPC.c (RS LDPC encode/RS_LDPC/RS_LDPC.c:221-431):
+// q = 2^s, M = gamma*q, N = rho*q.  gen_poly (rho-1 exponents, -1 = zero) and
+// coset (q*q entries) are the tables its H_pri=0 mode prints; either may be null.
+int build_rs_ldpc(int s, int rho, int gamma, HostGraph& g, std::vector<int>* gen_poly,
+                  std::vector<int>* coset, std::string* msg);
+
 }  // namespace ldpc

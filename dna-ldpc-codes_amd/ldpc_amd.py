@@ -61,6 +61,7 @@ _lib_lock = threading.Lock()
 
 EXPORTS = [
     "ldpc_abi_version", "ldpc_last_error", "ldpc_device_count", "ldpc_graph_load", "ldpc_graph_from_edges",
+    "ldpc_graph_load_alist", "ldpc_graph_rs_ldpc", "ldpc_graph_save_pchk", "ldpc_graph_save_alist",
     "ldpc_graph_free", "ldpc_graph_info", "ldpc_graph_edges", "ldpc_graph_syndrome", "ldpc_decode",
     "ldpc_engine_create", "ldpc_engine_create_ex", "ldpc_engine_info", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
     "ldpc_engine_gen_bsc", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
@@ -87,6 +88,12 @@ def lib():
         L.ldpc_graph_load.restype = vp
         L.ldpc_graph_from_edges.argtypes = [i32, i32, vp, vp, i64, pint]
         L.ldpc_graph_from_edges.restype = vp
+        L.ldpc_graph_load_alist.argtypes = [C.c_char_p, i32, pint]
+        L.ldpc_graph_load_alist.restype = vp
+        L.ldpc_graph_rs_ldpc.argtypes = [i32, i32, i32, vp, vp, pint]
+        L.ldpc_graph_rs_ldpc.restype = vp
+        L.ldpc_graph_save_pchk.argtypes = [vp, C.c_char_p]
+        L.ldpc_graph_save_alist.argtypes = [vp, C.c_char_p]
         L.ldpc_graph_free.argtypes = [vp]
         L.ldpc_graph_free.restype = None
         L.ldpc_graph_info.argtypes = [vp] + [vp] * 7
@@ -163,6 +170,39 @@ class Graph:
         if not h:
             raise LdpcError(err.value, (lib().ldpc_last_error() or b"").decode(errors="replace"))
         return cls(handle=h)
+
+    @classmethod
+    def from_alist(cls, path: str, transpose: bool = False) -> "Graph":
+        """alist file -> graph with alist-to-pchk's checks (alist-to-pchk.cpp:36-160)."""
+        err = C.c_int(0)
+        h = lib().ldpc_graph_load_alist(os.fsencode(path), int(bool(transpose)), C.byref(err))
+        if not h:
+            raise LdpcError(err.value, (lib().ldpc_last_error() or b"").decode(errors="replace"))
+        g = cls(handle=h)
+        g.path = path
+        return g
+
+    @classmethod
+    def rs_ldpc(cls, s: int, rho: int, gamma: int, tables: bool = False):
+        """RS-based LDPC code of RS_LDPC.c:221-431 (q = 2^s, M = gamma*q,
+        N = rho*q).  With tables=True also returns (gen_poly, coset)."""
+        q = 1 << s if 2 <= s <= 10 else 0
+        gp = np.zeros(max(rho - 1, 1), np.int32)
+        cs = np.zeros(max(q * q, 1), np.int32)
+        err = C.c_int(0)
+        h = lib().ldpc_graph_rs_ldpc(s, rho, gamma, _ptr(gp), _ptr(cs), C.byref(err))
+        if not h:
+            raise LdpcError(err.value, (lib().ldpc_last_error() or b"").decode(errors="replace"))
+        g = cls(handle=h)
+        return (g, gp[: rho - 1], cs[: q * q]) if tables else g
+
+    def save_pchk(self, path: str):
+        """Write a .pchk (intio magic + mod2sparse_write, mod2sparse.cpp:338-376)."""
+        _check(lib().ldpc_graph_save_pchk(self._h, os.fsencode(path)))
+
+    def save_alist(self, path: str):
+        """Write an alist file in RS_LDPC.c's layout (RS_LDPC.c:434-474)."""
+        _check(lib().ldpc_graph_save_alist(self._h, os.fsencode(path)))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -86,6 +86,25 @@ ldpc_graph *ldpc_graph_load(const char *pchk_path, int *err);
 ldpc_graph *ldpc_graph_from_edges(int32_t M, int32_t N, const int32_t *rows, const int32_t *cols,
                                   int64_t n_edges, int *err);
 
+/* Load an alist file with the rules of the reference's alist-to-pchk
+ * (alist-to-pchk.cpp:36-160); transpose != 0 is its -t option. */
+ldpc_graph *ldpc_graph_load_alist(const char *alist_path, int32_t transpose, int *err);
+
+/* Write the graph as a .pchk (intio_write magic + mod2sparse_write,
+ * mod2sparse.cpp:338-376) or as an alist file. */
+int ldpc_graph_save_pchk(const ldpc_graph *g, const char *pchk_path);
+int ldpc_graph_save_alist(const ldpc_graph *g, const char *alist_path);
+
+/* Build the RS-based LDPC code of RS_LDPC.c (RS LDPC encode/RS_LDPC/
+ * RS_LDPC.c:221-431): q = 2^s (2 <= s <= 10), M = gamma*q, N = rho*q,
+ * 3 <= rho <= q, 1 <= gamma <= q.  Optional outputs: gen_poly[rho-1]
+ * (generator polynomial exponents, -1 = zero) and coset[q*q] (coset number
+ * of every RS codeword, -1 = none) -- the tables its H_pri = 0 mode prints.
+ * The DNA code's decode_n18432_m2048_final.pchk is (8, 72, 8) with its
+ * columns permuted (tests/golden/rs_8_72_8_colperm.npz). */
+ldpc_graph *ldpc_graph_rs_ldpc(int32_t s, int32_t rho, int32_t gamma, int32_t *gen_poly,
+                               int32_t *coset, int *err);
+
 void ldpc_graph_free(ldpc_graph *g);
 
 /* Dimensions and degrees (CheckRegular, dec.cpp:138-189). */

@@ -140,6 +140,26 @@ def test_irregular_graph_generic_kernels(gpu, oracle_mod, tmp_path):
     _cmp(G, og, llr, 40, algo="msa")
 
 
+@pytest.mark.parametrize("code", [(5, 16, 4), (6, 32, 6), (7, 64, 8)])
+def test_rs_ldpc_codes_bitexact(gpu, oracle_mod, tmp_path, code):
+    """Codes from the native RS-LDPC constructor (RS_LDPC.c), written as
+    .pchk by the mod2sparse_write restatement and decoded on both sides."""
+    s, rho, gamma = code
+    g = gpu.Graph.rs_ldpc(s, rho, gamma)
+    path = tmp_path / f"rs_{s}_{rho}_{gamma}.pchk"
+    g.save_pchk(str(path))
+    og = oracle_mod.OracleGraph(str(path))
+    G = gpu.Graph(str(path))
+    assert (G.M, G.N, G.E, G.dc, G.dv) == (og.M, og.N, og.E, rho, gamma)
+    rng = np.random.default_rng(s)
+    # all-zero codeword through a BSC (p = 4%) plus a few erasures
+    flips = rng.random((96, G.N)) < 0.04
+    llr = np.where(flips, -synth.LLR_UNIT, synth.LLR_UNIT)
+    llr[:, ::97] = 0.0
+    _cmp(G, og, llr, 30)
+    _cmp(G, og, llr, 30, algo="msa")
+
+
 def _write_pchk(path, M, N, rows, cols):
     by_row = {}
     for r, c in zip(rows, cols):
