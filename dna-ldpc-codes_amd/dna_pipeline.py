@@ -93,6 +93,21 @@ def decode_trial(llr: np.ndarray, codewords: np.ndarray, eps: float = 0.02, max_
     }
 
 
+def trial_from_reads(reads, codewords: np.ndarray, eps: float = 0.02, max_iter: int = 200, align_fn=None,
+                     decode_fn: Optional[DecodeFn] = None, faithful: bool = True, device: int = 0) -> Dict:
+    """decoder.py:120-664 for one trial: reads (index values, payloads,
+    qualities) -> LLRs on the GPU (dna_llr.build_llr) -> first and second
+    decode.  Adds the LLR stage's time and strand statistics to the result."""
+    import dna_llr
+    t0 = time.perf_counter()
+    built = dna_llr.build_llr(*reads, eps=eps, align_fn=align_fn, device=device)
+    t_llr = time.perf_counter() - t0
+    res = decode_trial(built.llr, codewords, eps=eps, max_iter=max_iter, decode_fn=decode_fn, faithful=faithful)
+    res.update(t_llr_s=t_llr, n_erased_strands=int(len(built.erased)), n_reads_valid=built.n_reads_valid,
+               llr=built)
+    return res
+
+
 def report(res: Dict, rs: int = 72000) -> str:
     """The o_/x_ result-file body (decoder.py:668-727) without the wall time."""
     n = res["n"]

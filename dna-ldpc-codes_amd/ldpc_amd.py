@@ -65,7 +65,7 @@ EXPORTS = [
     "ldpc_graph_free", "ldpc_graph_info", "ldpc_graph_edges", "ldpc_graph_syndrome", "ldpc_decode",
     "ldpc_engine_create", "ldpc_engine_create_ex", "ldpc_engine_info", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
     "ldpc_engine_gen_bsc", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
-    "ldpc_dev_memcpy",
+    "ldpc_dev_memcpy", "ldpc_dna_llr", "ldpc_dna_edit_distance", "ldpc_write_soft_files", "ldpc_py_float_repr",
 ]
 
 

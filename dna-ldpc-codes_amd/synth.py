@@ -92,3 +92,96 @@ def bsc_llrs(codewords: np.ndarray, b0: int, B: int, seed: int, p: float, mag: f
     if as_lr:
         return np.where(y == 1, math.exp(-mag), math.exp(mag))
     return np.where(y == 1, -mag, mag)
+
+
+# --- sequenced reads for the LLR-construction stage -----
+DNA_FIXTURES = os.path.join(GOLDEN, "dna_fixtures.npz")
+_BASES = np.frombuffer(b"ACGT", np.uint8)
+
+
+def quality_hist() -> np.ndarray:
+    """Counts of per-read quality characters (ord) from the reference's
+    72000_RS_Q_{0..9}.txt (tests/golden/dna_fixtures.npz)."""
+    return np.load(DNA_FIXTURES, allow_pickle=False)["quality_hist"]
+
+
+def strand_payloads(codewords: np.ndarray) -> np.ndarray:
+    """[N][n_cw/2] uint8 ASCII: strand j's payload, nucleotide k = bits
+    (2k, 2k+1) of codewords (DNA2binary order, def_func.py:97-117)."""
+    bits = codewords.T.astype(np.int64)
+    return _BASES[2 * bits[:, 0::2] + bits[:, 1::2]]
+
+
+def dna_reads(codewords: np.ndarray, seed: int = 0, n_reads: int = 72000, sub: float = 0.01,
+              ins: float = 0.0, dele: float = 0.0, p_bad_index: float = 0.0,
+              quality: np.ndarray = None):
+    """Simulated random-sampled reads after index decoding: (index values,
+    payload strings, qualities).  Strand uniformly at random (the reference's
+    random sampling of `--rs` reads), per-base substitution / insertion /
+    deletion, a fraction of reads with a random (mostly invalid) 16-bit
+    index, quality = ord(char) drawn from the reference's quality histogram."""
+    import dna_llr
+    rng = np.random.default_rng(seed)
+    pay = strand_payloads(codewords)
+    N, nt = pay.shape
+    sidx = dna_llr.strand_indices()
+    strand = rng.integers(0, N, n_reads)
+    idx = sidx[strand].copy()
+    bad = rng.random(n_reads) < p_bad_index
+    idx[bad] = rng.integers(0, 1 << 16, int(bad.sum()))
+    qh = quality_hist() if quality is None else quality
+    qvals = np.nonzero(qh)[0]
+    quals = rng.choice(qvals, n_reads, p=qh[qvals] / qh[qvals].sum()).astype(np.int64)
+    r = pay[strand].copy()
+    m = rng.random(r.shape) < sub
+    r[m] = _BASES[(np.searchsorted(_BASES, r[m]) + rng.integers(1, 4, int(m.sum()))) % 4]
+    seqs = [row.tobytes().decode() for row in r]
+    if ins > 0 or dele > 0:
+        n_ins = rng.binomial(nt, ins, n_reads)
+        n_del = rng.binomial(nt, dele, n_reads)
+        for k in np.nonzero((n_ins > 0) | (n_del > 0))[0]:
+            s = list(seqs[k])
+            for _ in range(int(n_del[k])):
+                if s:
+                    del s[int(rng.integers(0, len(s)))]
+            for _ in range(int(n_ins[k])):
+                s.insert(int(rng.integers(0, len(s) + 1)), "ACGT"[int(rng.integers(0, 4))])
+            seqs[k] = "".join(s)
+    return idx.tolist(), seqs, quals.tolist()
+
+
+def dna_reads_edge_cases(codewords: np.ndarray, reads, seed: int = 1):
+    """Append reads that put the rarer per-strand shapes of decoder.py's loop
+    on fresh strands: single short read (q > 63 and q <= 63), single long
+    read, ragged strands with no close pair, ragged strands whose padded
+    alignment is not payload length (alignment failure), payload-length
+    ragged alignment, non-ACGT characters, and a bit-271 one-vs-one tie."""
+    import dna_llr
+    idx, seqs, quals = (list(x) for x in reads)
+    rng = np.random.default_rng(seed)
+    pay = strand_payloads(codewords)
+    sidx = dna_llr.strand_indices()
+    used = set(idx)
+    free = [j for j in rng.permutation(len(sidx)) if int(sidx[j]) not in used]
+    it = iter(free)
+
+    def add(j, s, q):
+        idx.append(int(sidx[j])); seqs.append(s); quals.append(int(q))
+
+    for q in (70, 60, 67):  # single short read
+        j = next(it); add(j, pay[j].tobytes().decode()[:100 + q % 7], q)
+    j = next(it); add(j, pay[j].tobytes().decode() + "ACG", 67)  # single long read
+    j = next(it)  # ragged, no close pair
+    add(j, "".join(rng.choice(list("ACGT"), 136)), 67); add(j, "".join(rng.choice(list("ACGT"), 120)), 67)
+    for _ in range(2):  # ragged, padded length 138 != 136 -> alignment failure (kind 3)
+        j = next(it); p = pay[j].tobytes().decode()
+        add(j, p + "GA", 67); add(j, p[:-1], 70); add(j, p[:-3] + "C", 40)
+    for _ in range(2):  # ragged, padded length 136 -> aligned rows counted
+        j = next(it); p = pay[j].tobytes().decode()
+        add(j, p, 67); add(j, p[:-2], 66); add(j, p[:130], 55)
+    j = next(it); p = pay[j].tobytes().decode()  # non-ACGT characters
+    add(j, p[:50] + "N" + p[51:], 67); add(j, p[:10] + "-" + p[11:], 67)
+    j = next(it); p = pay[j].tobytes().decode()  # tie at bit 271: one 0 vs one 1 among q >= 53
+    last = "A" if p[-1] in "CT" else "C"
+    add(j, p, 60); add(j, p[:-1] + last, 66); add(j, p, 40)
+    return idx, seqs, quals

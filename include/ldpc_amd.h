@@ -202,6 +202,41 @@ int ldpc_dev_free(int32_t device, void *p);
 int ldpc_dev_memcpy(int32_t device, void *dst, const void *src, size_t bytes, int32_t kind);
 
 /* ------------------------------------------------------------------------ */
+/* DNA soft-input construction (the step before the decoder)                 */
+/* ------------------------------------------------------------------------ */
+/* Per-strand LLRs from read candidates -- the arithmetic of decoder.py's
+ * strand loop (ex_decoder/decoder.py:142-519; count rule :266-320,
+ * :442-497).  The caller (dna_llr.py) classifies strand s into kind[s]:
+ *   0 no LLRs, 1 count over its rows, 2 one short candidate, 3 alignment
+ *   failed (count of the failed rows' last bases)
+ * and lays the candidate rows of strand s at rows[row_ptr[s]..row_ptr[s+1])
+ * (payload_nt bytes each, ASCII bases; for kinds 2 and 3 byte 0 of a row is
+ * the candidate's last base) with per-row quality row_q.  Output, on the
+ * host: llr[2*payload_nt][n_strands] (row i = soft file i+1, i.e. the
+ * decoder's [codeword][bit] layout) and optionally int_mask of the same
+ * shape (1 where the reference leaves an int 0, which str() prints as "0").
+ * Runs on `device`. */
+int ldpc_dna_llr(int32_t n_strands, const int32_t *kind, const int64_t *row_ptr, const uint8_t *rows,
+                 const int32_t *row_q, int32_t payload_nt, double llr_unit, double *llr, uint8_t *int_mask,
+                 int32_t device);
+
+/* Levenshtein distances of sequence pairs on `device`
+ * (def_func.edit_dist, def_func.py:10-26).  Sequence i is
+ * seqs[offsets[i] .. offsets[i]+lengths[i]); lengths <= 800. */
+int ldpc_dna_edit_distance(const uint8_t *seqs, const int64_t *offsets, const int32_t *lengths, int64_t n_seqs,
+                           const int32_t *pair_a, const int32_t *pair_b, int64_t n_pairs, int32_t *dist,
+                           int32_t device);
+
+/* Write soft<rs>_n18432_m1860_<i+1>.txt, i < n_files, into dir: row i of
+ * llr as str(value)+' ' tokens (decoder.py:511-516, def_func.py:54-57);
+ * int_mask (may be NULL) marks the int-0 entries.  Host only. */
+int ldpc_write_soft_files(const char *dir, int32_t rs, const double *llr, const uint8_t *int_mask,
+                          int32_t n_files, int32_t n_strands);
+
+/* Python repr() of a double into out (NUL-terminated); returns its length. */
+int ldpc_py_float_repr(double v, char *out, int32_t cap);
+
+/* ------------------------------------------------------------------------ */
 /* misc                                                                      */
 /* ------------------------------------------------------------------------ */
 const char *ldpc_last_error(void); /* thread-local message for the last failing call */
