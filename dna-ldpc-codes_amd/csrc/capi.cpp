@@ -244,11 +244,18 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
     if (!g) { set_error("null graph"); return LDPC_ERR_ARG; }
     if (B < 0 || max_iter < 0) { set_error("B and max_iter must be >= 0"); return LDPC_ERR_ARG; }
     if (B > 0 && (!llr || !hard_out)) { set_error("llr and hard_out are required"); return LDPC_ERR_ARG; }
-    if (algo != LDPC_ALGO_BP && algo != LDPC_ALGO_MSA) { set_error("unknown algorithm"); return LDPC_ERR_ARG; }
+    if (algo < LDPC_ALGO_BP || algo > LDPC_ALGO_GALLAGER_B2) { set_error("unknown algorithm"); return LDPC_ERR_ARG; }
     ldpc_opts o{};
     o.exp_on_host = 1;
     if (opts) o = *opts;
-    if (algo == LDPC_ALGO_MSA && post_out && o.post_kind == LDPC_POST_RATIO) {
+    // quantized min-sum parameters: 0 selects the engine defaults (q 6, step 0.5)
+    const int32_t q_prec = o.msa_precision > 0 ? o.msa_precision : 6;
+    const double q_step = o.msa_step > 0 ? o.msa_step : 0.5;
+    if (algo == LDPC_ALGO_QMSA && (q_prec < 2 || q_prec > 16 || o.msa_offset < 0)) {
+        set_error("quantized min-sum needs 2 <= msa_precision <= 16 and msa_offset >= 0");
+        return LDPC_ERR_ARG;
+    }
+    if (algo != LDPC_ALGO_BP && post_out && o.post_kind == LDPC_POST_RATIO) {
         set_error("LDPC_POST_RATIO is BP-only");
         return LDPC_ERR_ARG;
     }
@@ -291,6 +298,11 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
                 });
             auto step = [&]() -> int {
                 LDPC_HIP(hipSetDevice(dev));
+                if (algo == LDPC_ALGO_QMSA) {
+                    int r = E.set_params(q_prec, q_step, o.msa_offset, o.tie_seed);
+                    if (r) return r;
+                }
+                E.tie_base = b0;  // tie hash keyed by the codeword's index in this call
                 LDPC_HIP(hipMemcpyAsync(slot->d_in, slot->h_in, (size_t)Bc * N * 8, hipMemcpyHostToDevice, E.stream));
                 int r = E.decode(slot->d_in, in_kind, Bc, max_iter, slot->d_hard, post_out ? slot->d_post : nullptr,
                                     o.post_kind, slot->d_iters, slot->d_valid);
@@ -324,6 +336,13 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
     for (size_t i = 0; i < devs.size(); i++)
         if (rcs[i]) { set_error("device " + std::to_string(devs[i]) + ": " + msgs[i]); return rcs[i]; }
     return LDPC_OK;
+}
+
+int ldpc_engine_set_params(ldpc_engine* e, int32_t msa_precision, double msa_step, int32_t msa_offset,
+                           uint64_t tie_seed)
+{
+    if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
+    return e->e->set_params(msa_precision, msa_step, msa_offset, tie_seed);
 }
 
 ldpc_engine* ldpc_engine_create_ex(const ldpc_graph* g, int32_t device, int32_t algo, int64_t chunk,

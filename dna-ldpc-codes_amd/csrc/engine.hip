@@ -25,6 +25,7 @@
 
 #include "engine.hpp"
 #include "kernels.hpp"
+#include "kernels_int.hpp"
 
 #include <cstdlib>
 
@@ -92,7 +93,8 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     g = graph;
     device = dev;
     algo = algorithm;
-    if (algo != LDPC_ALGO_BP && algo != LDPC_ALGO_MSA) { set_error("unknown algorithm"); return LDPC_ERR_ARG; }
+    if (algo < LDPC_ALGO_BP || algo > LDPC_ALGO_GALLAGER_B2) { set_error("unknown algorithm"); return LDPC_ERR_ARG; }
+    const bool int_algo = algo >= LDPC_ALGO_QMSA;
     int ndev = 0;
     LDPC_HIP(hipGetDeviceCount(&ndev));
     if (dev < 0 || dev >= ndev) { set_error("device ordinal out of range"); return LDPC_ERR_DEVICE; }
@@ -142,7 +144,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         if ((rc = upload(&d_csc_pos, pos))) return rc;
     }
     if (cont_mode < 0) cont_mode = (int)env_int("LDPC_CONT", kDefaultCont);
-    cont = cont_mode != 0 && g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
+    cont = cont_mode != 0 && !int_algo && g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
     if (cont) {
         LDPC_HIP(hipMalloc((void**)&d_fresh, (size_t)cap_tiles * sizeof(uint64_t)));
         LDPC_HIP(hipMalloc((void**)&d_occ, (size_t)cap_tiles * sizeof(uint64_t)));
@@ -376,12 +378,99 @@ int Engine::run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_i
     return LDPC_OK;
 }
 
+int Engine::set_params(int32_t precision, double step, int32_t beta, uint64_t seed)
+{
+    if (precision < 2 || precision > 16 || !(step > 0) || beta < 0) {
+        set_error("quantized min-sum needs 2 <= precision <= 16, step > 0, offset >= 0");
+        return LDPC_ERR_ARG;
+    }
+    q_precision = precision;
+    q_step = step;
+    q_beta = beta;
+    tie_seed = seed;
+    return LDPC_OK;
+}
+
+// Integer-message decoders (kernels_int.hpp): fixed schedule, the same
+// syndrome / group loop as run_chunk on int32 views of the fp64 buffers.
+int Engine::run_chunk_int(const double* d_in, int64_t Bc, int64_t b_base, int32_t max_iter, uint8_t* d_hard,
+                          double* d_post, int32_t* d_iters, uint8_t* d_valid)
+{
+    using namespace dev;
+    const int32_t M = g->M, N = g->N;
+    const int64_t E = g->E;
+    const int64_t tiles = (Bc + 63) / 64;
+    IntParams ip{};
+    ip.algo = algo;
+    ip.max_value = (1 << (q_precision - 1)) - 1;  // Set_MSA dec.cpp:1688-1689
+    ip.min_value = -ip.max_value;
+    ip.beta = q_beta;
+    ip.step = q_step;
+    ip.seed = tie_seed;
+    b_base += tie_base;
+    const int dv = g->dv_max;  // D_v (CheckRegular)
+    if (algo == LDPC_ALGO_GALLAGER_A) { ip.b_var = dv - 1; ip.b_dec = dv; }
+    else if (algo == LDPC_ALGO_GALLAGER_B1) { ip.b_var = dv - 2; ip.b_dec = dv - 1; }
+    else { ip.b_var = dv / 2 + dv % 2; ip.b_dec = dv / 2 + 1; }
+    const bool reg_rowT = g->regular_dc && d_col_idx_T != nullptr;
+    if (d_post && !post_t) LDPC_HIP(hipMalloc((void**)&post_t, (size_t)cap * N * sizeof(double)));
+    double* pt = d_post ? post_t : nullptr;
+    int32_t* iv2c = reinterpret_cast<int32_t*>(v2c);
+    int32_t* ic2v = reinterpret_cast<int32_t*>(c2v);
+    int32_t* iprior = reinterpret_cast<int32_t*>(prior);
+    const dim3 blk(256);
+    const dim3 g_cols_all((N + 3) / 4, (unsigned)tiles);
+    LAUNCH(K_INIT, hipLaunchKernelGGL(k_init_int, dim3((N + 63) / 64, (unsigned)tiles), blk, 0, stream, d_in, Bc,
+                                      b_base, N, E, d_col_ptr, d_col_edge, ip, iprior, iv2c, hard, active, iters,
+                                      valid));
+    for (int32_t n = 0;; n++) {
+        if (reg_rowT && g->dc_max == 72)
+            LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome<72>, dim3((unsigned)tiles), dim3(1024), 0, stream, hard, active,
+                                             iters, valid, d_row_ptr, d_col_idx, d_col_idx_T, M, N, n, max_iter));
+        else
+            LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome<0>, dim3((unsigned)tiles), dim3(1024), 0, stream, hard, active,
+                                             iters, valid, d_row_ptr, d_col_idx, d_col_idx_T, M, N, n, max_iter));
+        if (n >= max_iter) break;
+        for (int64_t t0 = 0; t0 < tiles; t0 += group_tiles) {
+            const unsigned gt = (unsigned)std::min<int64_t>(group_tiles, tiles - t0);
+            LAUNCH(K_CHECK, hipLaunchKernelGGL(k_check_int, dim3((M + 3) / 4, gt), blk, 0, stream, iv2c, ic2v, active,
+                                               d_row_ptr, M, E, t0, ip));
+            LAUNCH(K_VAR, hipLaunchKernelGGL(k_var_int, dim3((N + 3) / 4, gt), blk, 0, stream, ic2v, iv2c, iprior,
+                                             hard, active, d_col_ptr, d_col_edge, pt, N, E, t0, b_base, n, ip));
+        }
+    }
+    if (d_post)
+        LAUNCH(K_FINAL, hipLaunchKernelGGL(k_finalize_int, g_cols_all, blk, 0, stream, post_t, iprior, iters, d_post,
+                                           Bc, N));
+    if (d_hard) {
+        const int64_t nblk = Bc * ((N + 255) / 256);
+        const unsigned grid = (unsigned)std::min<int64_t>(nblk, 1 << 20);
+        LAUNCH(K_FINAL, hipLaunchKernelGGL(k_unpack_hard, dim3(grid), blk, 0, stream, hard, d_hard, Bc, N));
+    }
+    if (d_iters) LDPC_HIP(hipMemcpyAsync(d_iters, iters, (size_t)Bc * sizeof(int32_t), hipMemcpyDeviceToDevice, stream));
+    if (d_valid) LDPC_HIP(hipMemcpyAsync(d_valid, valid, (size_t)Bc, hipMemcpyDeviceToDevice, stream));
+    return LDPC_OK;
+}
+
 int Engine::decode(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
                    int post_kind, int32_t* d_iters, uint8_t* d_valid)
 {
     if (B < 0 || max_iter < 0) { set_error("B and max_iter must be >= 0"); return LDPC_ERR_ARG; }
     if (B == 0) return LDPC_OK;
     LDPC_HIP(hipSetDevice(device));
+    if (algo >= LDPC_ALGO_QMSA) {
+        if (in_kind != LDPC_IN_LLR) { set_error("integer decoders take LLR input"); return LDPC_ERR_ARG; }
+        if (post_kind == LDPC_POST_RATIO && d_post) { set_error("LDPC_POST_RATIO is BP-only"); return LDPC_ERR_ARG; }
+        const size_t N = (size_t)g->N;
+        for (int64_t b0 = 0; b0 < B; b0 += cap) {
+            const int64_t Bc = std::min<int64_t>(cap, B - b0);
+            int rc = run_chunk_int(d_in + (size_t)b0 * N, Bc, b0, max_iter, d_hard ? d_hard + (size_t)b0 * N : nullptr,
+                                   d_post ? d_post + (size_t)b0 * N : nullptr, d_iters ? d_iters + b0 : nullptr,
+                                   d_valid ? d_valid + b0 : nullptr);
+            if (rc) return rc;
+        }
+        return LDPC_OK;
+    }
     if (cont) return run_cont(d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
     // balanced passes of <= cap codewords (multiples of 64 except the tail)
     const int64_t npass = (B + cap - 1) / cap;

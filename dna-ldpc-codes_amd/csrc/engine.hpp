@@ -68,6 +68,11 @@ struct Engine {
     int32_t* iters = nullptr;
     uint8_t* valid = nullptr;
     double* post_t = nullptr;  // [tiles][N][64] per-iteration posterior (allocated on first use)
+    // integer decoders (LDPC_ALGO_QMSA / GALLAGER_*): int32 views of v2c, c2v, prior
+    int32_t q_precision = 6, q_beta = 0;
+    double q_step = 0.5;
+    uint64_t tie_seed = 0;
+    int64_t tie_base = 0;  // added to the codeword index of the tie hash (host API: offset in the call)
     // profiling: HIP events around every `profile_stride`-th launch of a class
     int profile_stride = 0;
     int64_t sampled[K_NCLASS] = {0};
@@ -86,6 +91,10 @@ struct Engine {
                   int post_kind, int32_t* d_iters, uint8_t* d_valid);
     int decode(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
                int post_kind, int32_t* d_iters, uint8_t* d_valid);
+    // integer decoders, Bc <= cap codewords; b_base = global index of the first (tie hash)
+    int run_chunk_int(const double* d_in, int64_t Bc, int64_t b_base, int32_t max_iter, uint8_t* d_hard,
+                      double* d_post, int32_t* d_iters, uint8_t* d_valid);
+    int set_params(int32_t precision, double step, int32_t beta, uint64_t seed);
     int gen_bsc(double* d_out, int out_kind, int64_t b0, int64_t B, const uint8_t* d_cw, int32_t n_cw, uint64_t seed,
                 double p, double llr_mag);
     int collect_stats();

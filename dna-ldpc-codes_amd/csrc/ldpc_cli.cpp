@@ -6,8 +6,9 @@
 //        <EbNo | eps (BEC) | p (BSC)> <punct> <short> <target> [<VN0> <VN1> if target]
 //
 // Argument parsing follows SetUp (DNA_main.cpp:300-505) for this subset;
-// decoder_type 0 = BP (dec.cpp:583), 20 = float min-sum (dec.cpp:1216, with
-// g_precision = 0, DNA_main.cpp:1293-1296, 1588-1594).  Inputs: <codeword>.txt
+// decoder_type 0 = BP (dec.cpp:583), 20/21/22 = float min-sum (dec.cpp:1216,
+// with g_precision = 0, DNA_main.cpp:1293-1296, 1588-1594), 1/2/3 = Gallager
+// A/B1/B2 (dec.cpp:699).  Inputs: <codeword>.txt
 // (N ints, error statistics only), <soft>.txt (N LLRs, LR = exp(LLR),
 // DNA_main.cpp:1319-1345), <pchk>.pchk.  Outputs: dec_<codeword>.txt ("%d "
 // per bit, DNA_main.cpp:916-927), result_(<soft>.txt)_<pchk>.pchk_... .txt
@@ -79,9 +80,16 @@ int main(int argc, char** argv)
     if (punct != 0 || shortening != 0) die("ldpc: puncturing/shortening are not supported by this build");
     if (argc != pos) { std::fprintf(stderr, "\n\nargc error!\n\n"); return 1; }
     int algo;
+    // LDPC_Decode DNA_main.cpp:1565-1594.  The DNA build never sets
+    // g_precision (0), so 20/21/22 all run the float min-sum
+    // Run_MSA_Decoder_INF; Gallager 1/2/3 decode the hard decision of the
+    // soft input (the reference's DNA build leaves g_recv_codeword_hard unset).
     if (decoder_type == 0) algo = LDPC_ALGO_BP;
-    else if (decoder_type == 20) algo = LDPC_ALGO_MSA;
-    else die("ldpc: decoder_type must be 0 (BP) or 20 (min-sum)");
+    else if (decoder_type == 20 || decoder_type == 21 || decoder_type == 22) algo = LDPC_ALGO_MSA;
+    else if (decoder_type == 1) algo = LDPC_ALGO_GALLAGER_A;
+    else if (decoder_type == 2) algo = LDPC_ALGO_GALLAGER_B1;
+    else if (decoder_type == 3) algo = LDPC_ALGO_GALLAGER_B2;
+    else die("ldpc: decoder_type must be 0 (BP), 1/2/3 (Gallager A/B1/B2) or 20/21/22 (min-sum)");
     (void)eps; (void)p;
 
     const std::string file_cw = cw_base + ".txt", file_soft = soft_base + ".txt", file_pchk = pchk_base + ".pchk";

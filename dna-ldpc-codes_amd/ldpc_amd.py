@@ -29,13 +29,16 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libldpc_amd.so")
 
 LDPC_OK, LDPC_ERR_ARG, LDPC_ERR_IO, LDPC_ERR_FORMAT, LDPC_ERR_DEVICE, LDPC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
-ALGO_BP, ALGO_MSA = 0, 1
+ALGO_BP, ALGO_MSA, ALGO_QMSA, ALGO_GALLAGER_A, ALGO_GALLAGER_B1, ALGO_GALLAGER_B2 = 0, 1, 2, 3, 4, 5
 POST_LLR, POST_RATIO = 0, 1
 IN_LLR, IN_LR = 0, 1
 H2D, D2H, D2D = 0, 1, 2
 
 # reference decoder_type values (DNA_main.cpp:41-53)
-_ALGOS = {"bp": ALGO_BP, 0: ALGO_BP, "msa": ALGO_MSA, "min-sum": ALGO_MSA, 20: ALGO_MSA}
+# (ints are the ABI's LDPC_ALGO_* values; 20 = decoder_type MSA is also accepted)
+_ALGOS = {"bp": ALGO_BP, "msa": ALGO_MSA, "min-sum": ALGO_MSA, 20: ALGO_MSA, "qmsa": ALGO_QMSA,
+          "gallager_a": ALGO_GALLAGER_A, "gallager_b1": ALGO_GALLAGER_B1, "gallager_b2": ALGO_GALLAGER_B2,
+          **{k: k for k in range(6)}}
 
 
 class LdpcError(RuntimeError):
@@ -47,7 +50,8 @@ class LdpcError(RuntimeError):
 class Opts(C.Structure):
     _fields_ = [("n_devices", C.c_int32), ("devices", C.POINTER(C.c_int32)), ("chunk", C.c_int64),
                 ("exp_on_host", C.c_int32), ("post_kind", C.c_int32), ("host_threads", C.c_int32),
-                ("reserved", C.c_int32 * 7)]
+                ("msa_precision", C.c_int32), ("msa_offset", C.c_int32), ("reserved0", C.c_int32),
+                ("msa_step", C.c_double), ("tie_seed", C.c_uint64)]
 
 
 class KernelStats(C.Structure):
@@ -64,7 +68,7 @@ EXPORTS = [
     "ldpc_graph_load_alist", "ldpc_graph_rs_ldpc", "ldpc_graph_save_pchk", "ldpc_graph_save_alist",
     "ldpc_graph_free", "ldpc_graph_info", "ldpc_graph_edges", "ldpc_graph_syndrome", "ldpc_decode",
     "ldpc_engine_create", "ldpc_engine_create_ex", "ldpc_engine_info", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
-    "ldpc_engine_gen_bsc", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
+    "ldpc_engine_gen_bsc", "ldpc_engine_set_params", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
     "ldpc_dev_memcpy", "ldpc_dna_llr", "ldpc_dna_edit_distance", "ldpc_write_soft_files", "ldpc_py_float_repr",
 ]
 
@@ -113,6 +117,7 @@ def lib():
         L.ldpc_engine_stream.restype = vp
         L.ldpc_engine_gen_bsc.argtypes = [vp, vp, i32, i64, i64, vp, i32, C.c_uint64, dbl, dbl]
         L.ldpc_engine_profile.argtypes = [vp, i32]
+        L.ldpc_engine_set_params.argtypes = [vp, i32, dbl, i32, C.c_uint64]
         L.ldpc_engine_stats.argtypes = [vp, C.POINTER(KernelStats)]
         L.ldpc_dev_malloc.argtypes = [i32, C.c_size_t]
         L.ldpc_dev_malloc.restype = vp
@@ -140,7 +145,8 @@ def _algo(a) -> int:
     if isinstance(a, str):
         a = a.lower()
     if a not in _ALGOS:
-        raise ValueError(f"unknown algorithm {a!r} (use 'bp' or 'msa')")
+        raise ValueError(f"unknown algorithm {a!r} (use 'bp', 'msa', 'qmsa', 'gallager_a', 'gallager_b1', "
+                         "'gallager_b2')")
     return _ALGOS[a]
 
 
@@ -241,13 +247,15 @@ class Graph:
 
     def decode(self, llr: np.ndarray, max_iter: int = 200, algo="bp", post: Optional[str] = "llr",
                devices: Optional[Sequence[int]] = None, chunk: int = 0, exp_on_host: bool = True,
-               host_threads: int = 0):
+               host_threads: int = 0, msa_precision: int = 0, msa_step: float = 0.0, msa_offset: int = 0,
+               tie_seed: int = 0):
         """Decode a batch of LLR vectors ([B][N] or [N]) on the GPU(s).
 
         Returns (hard u8[B][N], post f64[B][N] or None, iters i32[B], valid bool[B]);
         a 1-D input returns 1-D / scalar outputs.  post: 'llr' (log of the BP
         posterior ratio / the min-sum L), 'ratio' (BP raw posterior ratio) or
-        None."""
+        None.  msa_* / tie_seed: parameters of algo='qmsa' (0 = defaults q 6,
+        step 0.5)."""
         a = _algo(algo)
         x = np.ascontiguousarray(llr, dtype=np.float64)
         single = x.ndim == 1
@@ -270,6 +278,8 @@ class Graph:
         o.exp_on_host = 1 if exp_on_host else 0
         o.post_kind = {None: POST_LLR, "llr": POST_LLR, "ratio": POST_RATIO}[post]
         o.host_threads = host_threads
+        o.msa_precision, o.msa_step, o.msa_offset, o.tie_seed = int(msa_precision), float(msa_step), int(msa_offset), \
+            int(tie_seed)
         _check(lib().ldpc_decode(self._h, _ptr(x), B, int(max_iter), a, _ptr(hard), _ptr(postv), _ptr(iters),
                                  _ptr(valid), C.byref(o)))
         valid = valid.astype(bool)
@@ -421,6 +431,10 @@ class Engine:
                d_iters=None, d_valid=None):
         _check(lib().ldpc_engine_decode(self._h, d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters,
                                         d_valid))
+
+    def set_params(self, msa_precision: int = 6, msa_step: float = 0.5, msa_offset: int = 0, tie_seed: int = 0):
+        """Quantized min-sum parameters (Set_MSA dec.cpp:1683)."""
+        _check(lib().ldpc_engine_set_params(self._h, msa_precision, msa_step, msa_offset, tie_seed))
 
     def gen_bsc(self, d_out, out_kind: int, b0: int, B: int, d_cw, n_cw: int, seed: int, p: float, llr_mag: float):
         _check(lib().ldpc_engine_gen_bsc(self._h, d_out, out_kind, b0, B, d_cw, n_cw, seed, p, llr_mag))

@@ -44,7 +44,17 @@ enum {
 /* decoder algorithms (reference decoder_type, DNA_main.cpp:49, 1565-1594) */
 enum {
     LDPC_ALGO_BP = 0,  /* sum-product, LR domain: Run_Belief_Propagation_Decoder dec.cpp:583 */
-    LDPC_ALGO_MSA = 1  /* float min-sum: Run_MSA_Decoder_INF dec.cpp:1216 (ldpc argv decoder_type 20) */
+    LDPC_ALGO_MSA = 1, /* float min-sum: Run_MSA_Decoder_INF dec.cpp:1216 (ldpc argv decoder_type 20) */
+    /* integer-message decoders of dec.cpp (not used by the DNA flow; LLR input):
+     * QMSA -- quantized min-sum Run_MSA_Decoder dec.cpp:1174 with q-bit messages,
+     *         quantizer step and offset beta (decoder_type 20/21 with g_precision > 0);
+     *         zero-posterior ties use a seeded counter hash instead of MKL rand_int(2)
+     * GALLAGER_* -- Run_Gallager_Decoder dec.cpp:699 type 0/1/2 (decoder_type 1/2/3)
+     *         on the hard decision of the input (LLR < 0 -> -1, else +1) */
+    LDPC_ALGO_QMSA = 2,
+    LDPC_ALGO_GALLAGER_A = 3,
+    LDPC_ALGO_GALLAGER_B1 = 4,
+    LDPC_ALGO_GALLAGER_B2 = 5
 };
 
 /* posterior output kinds (ldpc_opts.post_kind) */
@@ -69,7 +79,11 @@ typedef struct ldpc_opts {
                                DNA_main.cpp:1344 does (default 1 when opts == NULL) */
     int32_t post_kind;      /* LDPC_POST_* */
     int32_t host_threads;   /* threads for host exp/packing (0: auto) */
-    int32_t reserved[7];
+    int32_t msa_precision;  /* LDPC_ALGO_QMSA: message bits q, 2..16 (Set_MSA dec.cpp:1683) */
+    int32_t msa_offset;     /* LDPC_ALGO_QMSA: offset beta (1 = offset min-sum, decoder_type 21) */
+    int32_t reserved0;
+    double msa_step;        /* LDPC_ALGO_QMSA: quantizer step (g_step_length), > 0 */
+    uint64_t tie_seed;      /* LDPC_ALGO_QMSA: seed of the zero-posterior tie hash */
 } ldpc_opts;
 
 /* ------------------------------------------------------------------------ */
@@ -192,6 +206,10 @@ int ldpc_engine_profile(ldpc_engine *e, int32_t stride);
 
 /* The schedule an engine runs with: group tiles, nontemporal flag, resident
  * codewords per pass. */
+/* Parameters of LDPC_ALGO_QMSA (ignored by the other algorithms); the
+ * engine starts with q = 6, step = 0.5, beta = 0, seed = 0. */
+int ldpc_engine_set_params(ldpc_engine *e, int32_t msa_precision, double msa_step, int32_t msa_offset,
+                           uint64_t tie_seed);
 int ldpc_engine_info(ldpc_engine *e, int64_t *cap, int64_t *group_tiles, int32_t *flags);
 int ldpc_engine_stats(ldpc_engine *e, ldpc_kernel_stats *out);
 

@@ -414,3 +414,205 @@ int oracle_decode_batch(const oracle_graph *g, const double *llr, int64_t B, int
     free(th); free(jobs);
     return 0;
 }
+
+/* ------------------------------------------------------------------------ */
+/* integer-message decoders (dec.cpp:699-832, 1174-1210, 1256-1298,         */
+/* 1357-1396, 1438-1477, 1624-1764)                                          */
+/* ------------------------------------------------------------------------ */
+
+static uint64_t smix(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+/* stand-in for rand_int(2): stage 0 = Init_MSA, n+1 = Decision_MSA of iteration n */
+static int tie_bit(uint64_t seed, int64_t b, int stage, int j)
+{
+    uint64_t x = smix(seed);
+    x = smix(x ^ (uint64_t)b);
+    x = smix(x ^ (((uint64_t)(uint32_t)stage << 32) | (uint32_t)j));
+    return (int)(x & 1ull);
+}
+
+typedef struct {
+    int algo, max_value, min_value, beta, b_var, b_dec;
+    double step;
+    uint64_t seed;
+} int_params;
+
+/* Cal_MSA_Q(x, 0), dec.cpp:1708-1746 */
+static int cal_msa_q(double x, const int_params *p)
+{
+    int k, sign = x >= 0 ? 1 : -1;
+    double mag = fabs(x);
+    k = (int)(mag / p->step + 0.5);
+    if (sign == 1) {
+        if (k > p->max_value) k = p->max_value;
+    } else {
+        if (k > -p->min_value) k = -p->min_value;
+        k *= sign;
+    }
+    return k;
+}
+
+/* Cal_MSA_Clip, dec.cpp:1748-1764 */
+static int cal_msa_clip(int x, const int_params *p)
+{
+    if (x > p->max_value) return p->max_value;
+    if (x < p->min_value) return p->min_value;
+    return x;
+}
+
+/* one codeword; v2c/c2v indexed by CSR edge id */
+static int int_decode_one(const oracle_graph *g, const double *llr, int max_iter, const int_params *p, int64_t b,
+                          uint8_t *dblk, double *post, int *valid, int *prior, int *v2c, int *c2v)
+{
+    int N = g->N, M = g->M, n, c = 0;
+    /* Init_MSA dec.cpp:1256-1280 / Init_Gallager dec.cpp:725-739 */
+    for (int j = 0; j < N; j++) {
+        int m;
+        if (p->algo == 2) {
+            m = cal_msa_q(llr[j], p);
+            dblk[j] = m > 0 ? 0 : (m < 0 ? 1 : (uint8_t)tie_bit(p->seed, b, 0, j));
+        } else {
+            m = llr[j] < 0 ? -1 : 1;
+            dblk[j] = m >= 0 ? 0 : 1;
+        }
+        prior[j] = m;
+        post[j] = (double)m;
+        for (int q = g->col_ptr[j]; q < g->col_ptr[j + 1]; q++) v2c[g->col_edge[q]] = m;
+    }
+    for (n = 0;; n++) {
+        c = syndrome_rows(g, dblk);
+        if (n == max_iter || c == 0) break;
+        /* check phase: Check_Update_MSA dec.cpp:1357-1396 / Check_Update_Gallager :748-769 */
+        for (int i = 0; i < M; i++) {
+            for (int e = g->row_ptr[i]; e < g->row_ptr[i + 1]; e++) {
+                if (p->algo == 2) {
+                    int mag_min = -1, sign = 1;
+                    for (int f = g->row_ptr[i]; f < g->row_ptr[i + 1]; f++) {
+                        if (g->col_idx[e] == g->col_idx[f]) continue;
+                        int a = abs(v2c[f]);
+                        if (mag_min == -1 || mag_min > a) mag_min = a;
+                        sign *= v2c[f] >= 0 ? 1 : -1;
+                    }
+                    mag_min = mag_min - p->beta;
+                    if (mag_min < 0) mag_min = 0;
+                    c2v[e] = sign * mag_min;
+                } else {
+                    int temp = 1;
+                    for (int f = g->row_ptr[i]; f < g->row_ptr[i + 1]; f++)
+                        if (g->col_idx[e] != g->col_idx[f]) temp = temp * v2c[f];
+                    c2v[e] = temp;
+                }
+            }
+        }
+        /* variable phase + decision */
+        for (int j = 0; j < N; j++) {
+            int a0 = g->col_ptr[j], a1 = g->col_ptr[j + 1];
+            if (p->algo == 2) {
+                /* Variable_Update_MSA dec.cpp:1459-1476 */
+                for (int s = a0; s < a1; s++) {
+                    int e = g->col_edge[s], sum = prior[j];
+                    for (int r = a0; r < a1; r++)
+                        if (g->col_edge[r] != e) sum += c2v[g->col_edge[r]];
+                    v2c[e] = cal_msa_clip(sum, p);
+                }
+            } else {
+                /* Variable_Update_Gallager dec.cpp:771-802 */
+                int message = -prior[j];
+                for (int s = a0; s < a1; s++) {
+                    int e = g->col_edge[s], num = 0;
+                    for (int r = a0; r < a1; r++)
+                        if (g->col_edge[r] != e && c2v[g->col_edge[r]] == message) num++;
+                    v2c[e] = num >= p->b_var ? message : prior[j];
+                }
+            }
+        }
+        for (int j = 0; j < N; j++) {
+            int a0 = g->col_ptr[j], a1 = g->col_ptr[j + 1];
+            if (p->algo == 2) {
+                /* Decision_MSA dec.cpp:1624-1656 */
+                int sum = prior[j];
+                for (int s = a0; s < a1; s++) sum += c2v[g->col_edge[s]];
+                post[j] = (double)sum;
+                dblk[j] = sum > 0 ? 0 : (sum < 0 ? 1 : (uint8_t)tie_bit(p->seed, b, n + 1, j));
+            } else {
+                /* Decision_Gallager dec.cpp:804-832 */
+                int message = -prior[j], num = 0, temp;
+                for (int s = a0; s < a1; s++)
+                    if (c2v[g->col_edge[s]] == message) num++;
+                temp = num >= p->b_dec ? message : prior[j];
+                post[j] = (double)temp;
+                dblk[j] = temp >= 0 ? 0 : 1;
+            }
+        }
+    }
+    *valid = (c == 0);
+    return n;
+}
+
+typedef struct {
+    const oracle_graph *g;
+    const double *llr;
+    int64_t b0, b1;
+    int max_iter;
+    int_params p;
+    uint8_t *hard;
+    double *post;
+    int32_t *iters;
+    uint8_t *valid;
+} int_job_t;
+
+static void *int_worker(void *arg)
+{
+    int_job_t *jb = arg;
+    const oracle_graph *g = jb->g;
+    size_t N = (size_t)g->N, E = (size_t)(g->E ? g->E : 1);
+    int *prior = malloc(N * sizeof(int)), *v2c = malloc(E * sizeof(int)), *c2v = malloc(E * sizeof(int));
+    double *pb = malloc(N * sizeof(double));
+    for (int64_t b = jb->b0; b < jb->b1; b++) {
+        int valid = 0;
+        int n = int_decode_one(g, jb->llr + (size_t)b * N, jb->max_iter, &jb->p, b, jb->hard + (size_t)b * N, pb,
+                               &valid, prior, v2c, c2v);
+        if (jb->post) memcpy(jb->post + (size_t)b * N, pb, N * sizeof(double));
+        jb->iters[b] = n;
+        jb->valid[b] = (uint8_t)valid;
+    }
+    free(prior); free(v2c); free(c2v); free(pb);
+    return NULL;
+}
+
+int oracle_decode_int_batch(const oracle_graph *g, const double *llr, int64_t B, int max_iter, int algo,
+                            int precision, double step, int beta, uint64_t seed, int nthreads,
+                            uint8_t *hard, double *post, int32_t *iters, uint8_t *valid)
+{
+    int_params p;
+    int dv, rdv, dc, rdc;
+    if (algo < 2 || algo > 5 || (algo == 2 && (precision < 2 || precision > 16 || !(step > 0)))) return -1;
+    oracle_check_regular(g, &dv, &rdv, &dc, &rdc);
+    memset(&p, 0, sizeof p);
+    p.algo = algo;
+    p.max_value = (int)(pow(2.0, precision - 1) - 1); /* Set_MSA dec.cpp:1688-1689 */
+    p.min_value = -p.max_value;
+    p.beta = beta;
+    p.step = step;
+    p.seed = seed;
+    if (algo == 3) { p.b_var = dv - 1; p.b_dec = dv; }           /* dec.cpp:777-779, 810-812 */
+    else if (algo == 4) { p.b_var = dv - 2; p.b_dec = dv - 1; }
+    else { p.b_var = (dv / 2) + (dv % 2); p.b_dec = (dv / 2) + 1; }
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > B) nthreads = (int)(B > 0 ? B : 1);
+    pthread_t *th = malloc(sizeof(pthread_t) * (size_t)nthreads);
+    int_job_t *jobs = malloc(sizeof(int_job_t) * (size_t)nthreads);
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (int_job_t){g, llr, B * t / nthreads, B * (t + 1) / nthreads, max_iter, p, hard, post, iters, valid};
+        pthread_create(&th[t], NULL, int_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th); free(jobs);
+    return 0;
+}

@@ -18,6 +18,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ALGO_BP, ALGO_MSA = 0, 1
+ALGO_QMSA, ALGO_GALLAGER_A, ALGO_GALLAGER_B1, ALGO_GALLAGER_B2 = 2, 3, 4, 5
 POST_LLR, POST_RATIO = 0, 1
 
 
@@ -43,6 +44,9 @@ def lib():
         L.oracle_check.argtypes = [C.POINTER(_Graph), C.c_void_p, C.c_void_p]
         L.oracle_bp.argtypes = [C.POINTER(_Graph), C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
         L.oracle_msa.argtypes = [C.POINTER(_Graph), C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
+        L.oracle_decode_int_batch.argtypes = [C.POINTER(_Graph), C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int,
+                                              C.c_double, C.c_int, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, C.c_void_p]
         L.oracle_decode_batch.argtypes = [C.POINTER(_Graph), C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int,
                                           C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
@@ -118,6 +122,21 @@ class OracleGraph:
                                   _p(hard), _p(post) if post is not None else None, _p(iters), _p(valid))
         return hard, post, iters, valid
 
+    def decode_int_batch(self, llr: np.ndarray, max_iter: int, algo: int, precision: int = 6, step: float = 0.5,
+                         beta: int = 0, seed: int = 0, threads: int = 1):
+        """Integer decoders (algo 2 = quantized/offset min-sum, 3/4/5 =
+        Gallager A/B1/B2).  Returns (hard, post, iters, valid)."""
+        llr = np.ascontiguousarray(llr, dtype=np.float64)
+        B = llr.shape[0]
+        hard = np.zeros((B, self.N), np.uint8)
+        post = np.zeros((B, self.N), np.float64)
+        iters = np.zeros(B, np.int32)
+        valid = np.zeros(B, np.uint8)
+        rc = lib().oracle_decode_int_batch(C.byref(self._g), _p(llr), B, max_iter, algo, precision, step, beta, seed,
+                                           threads, _p(hard), _p(post), _p(iters), _p(valid))
+        if rc != 0:
+            raise ValueError("bad integer-decoder parameters")
+        return hard, post, iters, valid
 
 # ---------------------------------------------------------------------------
 # oracle/_ref: the reference's own loader + syndrome (built only where the
