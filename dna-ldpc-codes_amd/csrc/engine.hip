@@ -36,6 +36,8 @@ constexpr int64_t kDefaultNT = 1;
 constexpr int64_t kDefaultPipe = 0;
 constexpr int64_t kDefaultCsc = 0;
 constexpr int64_t kDefaultCont = 1;
+constexpr int64_t kDefaultC2vProbe = 4;  // LDPC_C2V_PROBE: candidate c2v scratch buffers timed at init
+constexpr int64_t kDefaultVarCpw = 8;  // LDPC_VAR_CPW (A/B: +3.8% over 1 column per wave)
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
@@ -143,6 +145,8 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         for (size_t q = 0; q < g->col_edge.size(); q++) pos[(size_t)g->col_edge[q]] = (int32_t)q;
         if ((rc = upload(&d_csc_pos, pos))) return rc;
     }
+    var_cpw = (int)env_int("LDPC_VAR_CPW", kDefaultVarCpw);
+    if (var_cpw != 1 && var_cpw != 2 && var_cpw != 4 && var_cpw != 8) var_cpw = 1;
     if (cont_mode < 0) cont_mode = (int)env_int("LDPC_CONT", kDefaultCont);
     cont = cont_mode != 0 && !int_algo && g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
     if (cont) {
@@ -166,7 +170,61 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     LDPC_HIP(hipMalloc((void**)&active, (size_t)cap_tiles * sizeof(uint64_t)));
     LDPC_HIP(hipMalloc((void**)&iters, (size_t)cap * sizeof(int32_t)));
     LDPC_HIP(hipMalloc((void**)&valid, (size_t)cap * sizeof(uint8_t)));
+    const int probes = (int)env_int("LDPC_C2V_PROBE", kDefaultC2vProbe);
+    if (probes > 1 && !int_algo && group_tiles < cap_tiles) return probe_c2v(probes);
     return LDPC_OK;
+}
+
+// The check->variable scratch of one tile group (~226 MB at G = 3) is meant
+// to stay in the 256 MB Infinity Cache, a memory-side cache whose slices
+// belong to HBM channels: how well a given allocation fits depends on where
+// its physical pages land, and identical engines were measured 3-4 % apart.
+// Allocate `probes` candidate scratch buffers, time one real check+variable
+// step of a tile group on each (state zeroed, results discarded -- every
+// decode re-initialises), keep the fastest.
+int Engine::probe_c2v(int probes)
+{
+    const size_t E = (size_t)std::max<int64_t>(g->E, 1);
+    const size_t bytes = (size_t)c2v_tiles * 64 * E * sizeof(double);
+    const unsigned gt = (unsigned)std::min<int64_t>(group_tiles, cap_tiles);
+    LDPC_HIP(hipMemsetAsync(v2c, 0, (size_t)gt * 64 * E * sizeof(double), stream));
+    LDPC_HIP(hipMemsetAsync(prior, 0, (size_t)gt * 64 * g->N * sizeof(double), stream));
+    LDPC_HIP(hipMemsetAsync(active, 0xff, (size_t)gt * sizeof(uint64_t), stream));
+    std::vector<double*> cand{c2v};
+    for (int i = 1; i < probes; i++) {
+        double* p = nullptr;
+        if (hipMalloc((void**)&p, bytes) != hipSuccess) { (void)hipGetLastError(); break; }
+        cand.push_back(p);
+    }
+    hipEvent_t e0, e1;
+    LDPC_HIP(hipEventCreate(&e0));
+    LDPC_HIP(hipEventCreate(&e1));
+    const int saved_stride = profile_stride;
+    profile_stride = 0;
+    size_t best = 0;
+    float best_ms = 1e30f;
+    int rc = LDPC_OK;
+    for (size_t c = 0; c < cand.size() && rc == LDPC_OK; c++) {
+        for (int rep = 0; rep < 4 && rc == LDPC_OK; rep++) {  // rep 0 warms up
+            if (rep == 1 && hipEventRecord(e0, stream) != hipSuccess) rc = LDPC_ERR_DEVICE;
+            if (!rc) rc = launch_check(stream, cand[c], 0, gt);
+            if (!rc) rc = launch_var(stream, cand[c], 0, gt, nullptr, dev::Refill{});
+        }
+        if (rc) break;
+        LDPC_HIP(hipEventRecord(e1, stream));
+        LDPC_HIP(hipEventSynchronize(e1));
+        float ms = 0;
+        LDPC_HIP(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best_ms) { best_ms = ms; best = c; }
+    }
+    profile_stride = saved_stride;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    for (size_t c = 0; c < cand.size(); c++)
+        if (c != best) (void)hipFree(cand[c]);
+    c2v = cand[best];
+    for (int k = 0; k < K_NCLASS; k++) launches[k] = 0;
+    return rc;
 }
 
 hipEvent_t Engine::get_event()
@@ -255,6 +313,29 @@ static void var_regular3(int algo, hipStream_t s, dim3 grid, const double* scrat
                            col_edge, pt, N, E, t0, rf);
 }
 
+template <int CPW>
+static void var_bp_multi2(hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior, uint64_t* hard,
+                          const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E, int64_t t0,
+                          const dev::Refill& rf)
+{
+    using namespace dev;
+    if (rf.fresh)
+        hipLaunchKernelGGL((k_var_bp_m<8, true, true, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
+                           col_edge, pt, N, E, t0, rf);
+    else
+        hipLaunchKernelGGL((k_var_bp_m<8, true, false, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
+                           col_edge, pt, N, E, t0, rf);
+}
+
+static void var_bp_multi(int cpw, hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior,
+                         uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N,
+                         int64_t E, int64_t t0, const dev::Refill& rf)
+{
+    if (cpw == 2) var_bp_multi2<2>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+    else if (cpw == 4) var_bp_multi2<4>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+    else var_bp_multi2<8>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+}
+
 template <bool NT, bool CSCL>
 static void var_regular(int algo, hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior,
                         uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N,
@@ -294,6 +375,11 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
     const int64_t E = g->E;
     const bool reg8 = g->regular_dv && g->dv_max == 8;
     const dim3 grid((N + 3) / 4, gt), blk(256);
+    if (reg8 && var_cpw > 1 && algo == LDPC_ALGO_BP && nt_d && !lr_csc && N % (4 * var_cpw) == 0) {
+        const dim3 gm((unsigned)(N / (4 * var_cpw)), gt);
+        LAUNCH_ON(s, K_VAR, var_bp_multi(var_cpw, s, gm, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf));
+        return LDPC_OK;
+    }
     if (reg8) {
         // lr_csc implies both phases use the regular kernels
         LAUNCH_ON(s, K_VAR, {

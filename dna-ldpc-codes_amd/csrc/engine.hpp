@@ -42,6 +42,7 @@ struct Engine {
     bool pipe = false;        // check(g+1) on `stream` overlaps variable(g) on `stream2`
     bool lr_csc = false;      // c2v scratch in column (CSC) order (regular kernels only)
     bool cont = false;        // continuous batching: refill lanes as codewords finish
+    int var_cpw = 1;          // BP variable phase: columns per wave (k_var_bp_m when > 1)
     static constexpr int kRing = 8, kLag = 2;
     uint64_t* d_fresh = nullptr;
     uint64_t* d_occ = nullptr;
@@ -103,6 +104,7 @@ struct Engine {
     hipEvent_t get_event();
     int mark_begin(KClass c, hipStream_t s, hipEvent_t* b);
     int mark_end(KClass c, hipStream_t s, hipEvent_t b);
+    int probe_c2v(int probes);
     int launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt);
     int launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt, const dev::Refill& rf);
 };

@@ -350,6 +350,85 @@ __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, d
     }
 }
 
+// Same variable phase, CPW consecutive columns per wave: every lr load of
+// the wave's columns is issued before the first column's products, fewer
+// and longer-lived waves.  Requires N % (4 * CPW) == 0.
+template <int DV, bool NT, bool CONT, int CPW>
+__global__ __launch_bounds__(256) void k_var_bp_m(const double* __restrict__ lr, double* __restrict__ dmsg,
+                                                  double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                                  const uint64_t* __restrict__ active,
+                                                  const int32_t* __restrict__ col_edge, double* __restrict__ post,
+                                                  int32_t N, int64_t E, int64_t t0, Refill rf)
+{
+    const int lane = lane_id();
+    const int32_t j0 = (xcd_block(blockIdx.x, gridDim.x) * 4 + wave_id()) * CPW;
+    const int64_t t = t0 + blockIdx.y;
+    if (j0 >= N) return;
+    const uint64_t act = active[t];
+    const uint64_t frm = CONT ? rf.fresh[t] : 0ull;
+    const uint64_t touched = act | frm;
+    if (touched == 0) return;
+    const bool live = (act >> lane) & 1ull;
+    const bool fr = CONT && ((frm >> lane) & 1ull);
+    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
+    int32_t eid[CPW][DV];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c)
+#pragma unroll
+        for (int s = 0; s < DV; ++s) eid[c][s] = col_edge[(size_t)(j0 + c) * DV + s];
+    double l[CPW][DV], LR[CPW];
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) {
+            LR[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
+#pragma unroll
+            for (int s = 0; s < DV; ++s) l[c][s] = lr[(tl + (size_t)eid[c][s]) * TILE + lane];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        const int32_t j = j0 + c;
+        const size_t pj = ((size_t)t * N + j) * TILE + lane;
+        bool h = false;
+        double dv[DV];
+        if (fr) {
+            const double x = rf.in[(size_t)rf.lane_b[t * TILE + lane] * N + j];
+            const double LR0 = rf.in_is_llr ? exp(x) : x;
+            prior[pj] = LR0;
+            const double d0 = 1.0 - 2.0 / (1.0 + LR0);
+#pragma unroll
+            for (int s = 0; s < DV; ++s) dv[s] = d0;
+            h = (LR0 < 1.0);
+        } else if (live) {
+            double pr[DV];
+            double p = LR[c];
+#pragma unroll
+            for (int s = 0; s < DV; ++s) { pr[s] = p; p = p * l[c][s]; }
+            if (__builtin_isnan(p)) p = 1.0;
+            h = (p <= 1.0);
+            if (post) post[pj] = p;
+            double acc = 1.0;
+#pragma unroll
+            for (int s = DV - 1; s >= 0; --s) {
+                double v = pr[s] * acc;
+                if (__builtin_isnan(v)) v = 1.0;
+                acc = acc * l[c][s];
+                dv[s] = 1.0 - 2.0 / (1.0 + v);
+            }
+        }
+        if (fr || live) {
+#pragma unroll
+            for (int s = 0; s < DV; ++s) st<NT>(dmsg + (tb + eid[c][s]) * TILE + lane, dv[s]);
+        }
+        const uint64_t m = __ballot(h);
+        if (lane == 0) {
+            const size_t o = (size_t)t * N + j;
+            const uint64_t old = (touched == ~0ull) ? 0ull : hard[o];
+            hard[o] = (old & ~touched) | (m & touched);
+        }
+    }
+}
+
 // Generic column degree: the partial products go through the v2c array
 // exactly as the reference keeps them in e->pr.
 __global__ __launch_bounds__(256) void k_var_bp_gen(const double* __restrict__ lr, double* __restrict__ dmsg,

@@ -248,6 +248,20 @@ def test_grouped_schedules_bitexact(gpu, og, codewords, monkeypatch, group, nt, 
     _cmp(G2, og, llr, 30, algo="msa")
 
 
+@pytest.mark.parametrize("cpw,cont", [(2, 0), (4, 1), (8, 0), (2, 1)])
+def test_variable_columns_per_wave_bitexact(gpu, og, codewords, monkeypatch, cpw, cont):
+    """k_var_bp_m (CPW columns per wave) changes only which wave handles a
+    column, never a column's arithmetic; with continuous batching its
+    refill path initialises fresh lanes."""
+    monkeypatch.setenv("LDPC_VAR_CPW", str(cpw))
+    monkeypatch.setenv("LDPC_CONT", str(cont))
+    G2 = gpu.Graph(PCHK)
+    llr = synth.dna_like_llrs(codewords, seed=3, reads=57000)[:200]
+    _cmp(G2, og, llr, 60)
+    llr = synth.bsc_llrs(codewords, 0, 150, seed=7, p=0.004)
+    _cmp(G2, og, llr, 40)
+
+
 @pytest.mark.parametrize("chunk", [64, 128])
 def test_continuous_batching_edge_cases(gpu, og, codewords, monkeypatch, chunk):
     """Continuous mode with a pool smaller than the batch (lanes are refilled

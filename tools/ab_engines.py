@@ -1,0 +1,90 @@
+"""In-process A/B timing of engine variants on the same device-resident
+workload (the bench's BSC config 3 input), alternating variants so clock,
+thermal and allocation effects hit both alike.
+
+    python tools/ab_engines.py --var A:LDPC_VAR_CPW=1 --var B:LDPC_VAR_CPW=8 --reps 6
+
+Each variant is NAME:ENV=VAL[,ENV=VAL...]; the env is applied while that
+variant's engine is created (the engine reads it at init).  Prints one JSON
+line per variant with the median/min seconds per decode and cw/s.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dna-ldpc-codes_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--var", action="append", required=True)
+    ap.add_argument("--batch", type=int, default=32768)
+    ap.add_argument("--max-iter", type=int, default=50)
+    ap.add_argument("--algo", default="bp")
+    ap.add_argument("--p", type=float, default=0.02)
+    ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--chunk", type=int, default=16384)
+    ap.add_argument("--profile", type=int, default=0, help="HIP-event sample stride per kernel class (0: off)")
+    args = ap.parse_args()
+    import ldpc_amd as L
+    import synth
+    G = L.Graph(synth.PCHK)
+    cw = synth.load_codewords()
+    B, N = args.batch, G.N
+    d_cw = L.DeviceBuffer(0, cw.size)
+    d_cw.upload(np.ascontiguousarray(cw))
+    d_in = L.DeviceBuffer(0, B * N * 8)
+    d_h, d_i, d_v = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
+    engines = []
+    for spec in args.var:
+        name, _, envs = spec.partition(":")
+        saved = {}
+        for kv in filter(None, envs.split(",")):
+            k, v = kv.split("=", 1)
+            saved[k] = os.environ.get(k)
+            os.environ[k] = v
+        e = L.Engine(G, 0, args.algo, chunk=args.chunk)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        if args.profile:
+            e.profile(args.profile)
+        engines.append((name, e))
+    engines[0][1].gen_bsc(d_in.at(0), L.IN_LLR, 0, B, d_cw.at(0), cw.shape[0], 2026, args.p, synth.LLR_UNIT)
+    engines[0][1].sync()
+    times = {n: [] for n, _ in engines}
+    ref = None
+    for rep in range(args.reps + 1):
+        for name, e in engines:
+            t = time.perf_counter()
+            e.decode(d_in.at(0), L.IN_LLR, B, args.max_iter, d_h.at(0), None, L.POST_LLR, d_i.at(0), d_v.at(0))
+            e.sync()
+            el = time.perf_counter() - t
+            if rep > 0:
+                times[name].append(el)
+            it = d_i.download(np.empty(B, np.int32))
+            if ref is None:
+                ref = it.copy()
+            elif not np.array_equal(ref, it):
+                raise SystemExit(f"variant {name} changed the iteration counts")
+        print(json.dumps({"rep": rep, **{n: round(B / v[-1], 1) for n, v in times.items() if v}}), flush=True)
+    for name, e in engines:
+        if args.profile:
+            st = e.stats()
+            print(json.dumps({"variant": name, "kernels": {k: {"launches": v["launches"], "avg_ms": round(
+                v["ms"] / max(v["sampled"], 1), 4)} for k, v in st.items() if v["launches"]}}), flush=True)
+    for name, v in times.items():
+        print(json.dumps({"variant": name, "median_s": round(float(np.median(v)), 5), "min_s": round(min(v), 5),
+                          "cw_per_s_median": round(B / float(np.median(v)), 1), "cw_per_s_best": round(B / min(v), 1),
+                          "reps": len(v)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
