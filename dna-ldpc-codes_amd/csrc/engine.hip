@@ -37,7 +37,7 @@ constexpr int64_t kDefaultPipe = 0;
 constexpr int64_t kDefaultCsc = 0;
 constexpr int64_t kDefaultCont = 1;
 constexpr int64_t kDefaultC2vProbe = 4;  // LDPC_C2V_PROBE: candidate c2v scratch buffers timed at init
-constexpr int64_t kDefaultVarCpw = 8;  // LDPC_VAR_CPW (A/B: +3.8% over 1 column per wave)
+constexpr int64_t kDefaultVarCpw = 4;  // LDPC_VAR_CPW (A/B over two boxes: +2.6-2.9% over 1 column per wave)
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }

@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--chunk", type=int, default=16384)
     ap.add_argument("--profile", type=int, default=0, help="HIP-event sample stride per kernel class (0: off)")
+    ap.add_argument("--fresh", type=int, default=0,
+                    help="rounds of create/time/free per variant (averages allocation placement); 0 = one "
+                         "engine per variant, timed --reps times")
     args = ap.parse_args()
     import ldpc_amd as L
     import synth
@@ -40,6 +43,55 @@ def main():
     d_cw.upload(np.ascontiguousarray(cw))
     d_in = L.DeviceBuffer(0, B * N * 8)
     d_h, d_i, d_v = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
+    def make(spec):
+        name, _, envs = spec.partition(":")
+        saved = {}
+        for kv in filter(None, envs.split(",")):
+            k, v = kv.split("=", 1)
+            saved[k] = os.environ.get(k)
+            os.environ[k] = v
+        e = L.Engine(G, 0, args.algo, chunk=args.chunk)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        return name, e
+
+    if args.fresh:
+        gen = None
+        res = {}
+        ref = None
+        for rnd in range(args.fresh):
+            # rotate the creation order: the allocator hands out the same
+            # memory to the same creation slot, so every variant visits every slot
+            k0 = rnd % len(args.var)
+            for spec in args.var[k0:] + args.var[:k0]:
+                name, e = make(spec)
+                if gen is None:
+                    e.gen_bsc(d_in.at(0), L.IN_LLR, 0, B, d_cw.at(0), cw.shape[0], 2026, args.p, synth.LLR_UNIT)
+                    gen = True
+                ts = []
+                for k in range(2):  # warm-up + timed
+                    t = time.perf_counter()
+                    e.decode(d_in.at(0), L.IN_LLR, B, args.max_iter, d_h.at(0), None, L.POST_LLR, d_i.at(0),
+                             d_v.at(0))
+                    e.sync()
+                    ts.append(time.perf_counter() - t)
+                it = d_i.download(np.empty(B, np.int32))
+                if ref is None:
+                    ref = it.copy()
+                elif not np.array_equal(ref, it):
+                    raise SystemExit(f"variant {name} changed the iteration counts")
+                res.setdefault(name, []).append(B / ts[1])
+                del e
+            print(json.dumps({"round": rnd, **{n: round(v[-1], 1) for n, v in res.items()}}), flush=True)
+        for name, v in res.items():
+            print(json.dumps({"variant": name, "cw_per_s_mean": round(float(np.mean(v)), 1),
+                              "cw_per_s_std": round(float(np.std(v)), 1), "cw_per_s_min": round(min(v), 1),
+                              "cw_per_s_max": round(max(v), 1), "rounds": len(v)}), flush=True)
+        return
+
     engines = []
     for spec in args.var:
         name, _, envs = spec.partition(":")
