@@ -313,27 +313,36 @@ static void var_regular3(int algo, hipStream_t s, dim3 grid, const double* scrat
                            col_edge, pt, N, E, t0, rf);
 }
 
-template <int CPW>
-static void var_bp_multi2(hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior, uint64_t* hard,
-                          const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E, int64_t t0,
-                          const dev::Refill& rf)
+template <bool MSA, int CPW>
+static void var_multi2(hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior, uint64_t* hard,
+                       const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E, int64_t t0,
+                       const dev::Refill& rf)
 {
     using namespace dev;
     if (rf.fresh)
-        hipLaunchKernelGGL((k_var_bp_m<8, true, true, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
+        hipLaunchKernelGGL((k_var_m<MSA, 8, true, true, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
                            col_edge, pt, N, E, t0, rf);
     else
-        hipLaunchKernelGGL((k_var_bp_m<8, true, false, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
+        hipLaunchKernelGGL((k_var_m<MSA, 8, true, false, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
                            col_edge, pt, N, E, t0, rf);
 }
 
-static void var_bp_multi(int cpw, hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior,
-                         uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N,
-                         int64_t E, int64_t t0, const dev::Refill& rf)
+template <bool MSA>
+static void var_multi1(int cpw, hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior,
+                       uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E,
+                       int64_t t0, const dev::Refill& rf)
 {
-    if (cpw == 2) var_bp_multi2<2>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
-    else if (cpw == 4) var_bp_multi2<4>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
-    else var_bp_multi2<8>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+    if (cpw == 2) var_multi2<MSA, 2>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+    else if (cpw == 4) var_multi2<MSA, 4>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+    else var_multi2<MSA, 8>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+}
+
+static void var_multi(int algo, int cpw, hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior,
+                      uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E,
+                      int64_t t0, const dev::Refill& rf)
+{
+    if (algo == LDPC_ALGO_MSA) var_multi1<true>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+    else var_multi1<false>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
 }
 
 template <bool NT, bool CSCL>
@@ -375,9 +384,9 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
     const int64_t E = g->E;
     const bool reg8 = g->regular_dv && g->dv_max == 8;
     const dim3 grid((N + 3) / 4, gt), blk(256);
-    if (reg8 && var_cpw > 1 && algo == LDPC_ALGO_BP && nt_d && !lr_csc && N % (4 * var_cpw) == 0) {
+    if (reg8 && var_cpw > 1 && nt_d && !lr_csc && N % (4 * var_cpw) == 0) {
         const dim3 gm((unsigned)(N / (4 * var_cpw)), gt);
-        LAUNCH_ON(s, K_VAR, var_bp_multi(var_cpw, s, gm, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf));
+        LAUNCH_ON(s, K_VAR, var_multi(algo, var_cpw, s, gm, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf));
         return LDPC_OK;
     }
     if (reg8) {

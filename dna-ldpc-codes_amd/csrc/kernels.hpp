@@ -350,15 +350,16 @@ __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, d
     }
 }
 
-// Same variable phase, CPW consecutive columns per wave: every lr load of
-// the wave's columns is issued before the first column's products, fewer
-// and longer-lived waves.  Requires N % (4 * CPW) == 0.
-template <int DV, bool NT, bool CONT, int CPW>
-__global__ __launch_bounds__(256) void k_var_bp_m(const double* __restrict__ lr, double* __restrict__ dmsg,
-                                                  double* __restrict__ prior, uint64_t* __restrict__ hard,
-                                                  const uint64_t* __restrict__ active,
-                                                  const int32_t* __restrict__ col_edge, double* __restrict__ post,
-                                                  int32_t N, int64_t E, int64_t t0, Refill rf)
+// Variable phase, CPW consecutive columns per wave, BP (MSA = false, the
+// arithmetic of k_var_bp) or min-sum (MSA = true, that of k_var_msa): every
+// c2v load of the wave's columns is issued before the first column's
+// arithmetic -- fewer, longer-lived waves.  Requires N % (4 * CPW) == 0.
+template <bool MSA, int DV, bool NT, bool CONT, int CPW>
+__global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, double* __restrict__ v2c,
+                                               double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                               const uint64_t* __restrict__ active,
+                                               const int32_t* __restrict__ col_edge, double* __restrict__ post,
+                                               int32_t N, int64_t E, int64_t t0, Refill rf)
 {
     const int lane = lane_id();
     const int32_t j0 = (xcd_block(blockIdx.x, gridDim.x) * 4 + wave_id()) * CPW;
@@ -376,13 +377,13 @@ __global__ __launch_bounds__(256) void k_var_bp_m(const double* __restrict__ lr,
     for (int c = 0; c < CPW; ++c)
 #pragma unroll
         for (int s = 0; s < DV; ++s) eid[c][s] = col_edge[(size_t)(j0 + c) * DV + s];
-    double l[CPW][DV], LR[CPW];
+    double l[CPW][DV], pv[CPW];
     if (live) {
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
-            LR[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
+            pv[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
 #pragma unroll
-            for (int s = 0; s < DV; ++s) l[c][s] = lr[(tl + (size_t)eid[c][s]) * TILE + lane];
+            for (int s = 0; s < DV; ++s) l[c][s] = c2v[(tl + (size_t)eid[c][s]) * TILE + lane];
         }
     }
 #pragma unroll
@@ -391,34 +392,57 @@ __global__ __launch_bounds__(256) void k_var_bp_m(const double* __restrict__ lr,
         const size_t pj = ((size_t)t * N + j) * TILE + lane;
         bool h = false;
         double dv[DV];
-        if (fr) {
+        if (fr) {  // Init_Belief_Propagation / Init_MSA_INF for a refilled lane
             const double x = rf.in[(size_t)rf.lane_b[t * TILE + lane] * N + j];
-            const double LR0 = rf.in_is_llr ? exp(x) : x;
-            prior[pj] = LR0;
-            const double d0 = 1.0 - 2.0 / (1.0 + LR0);
+            if (MSA) {
+                prior[pj] = x;
 #pragma unroll
-            for (int s = 0; s < DV; ++s) dv[s] = d0;
-            h = (LR0 < 1.0);
+                for (int s = 0; s < DV; ++s) dv[s] = x;
+                h = !(x > 0);
+            } else {
+                const double LR0 = rf.in_is_llr ? exp(x) : x;
+                prior[pj] = LR0;
+                const double d0 = 1.0 - 2.0 / (1.0 + LR0);
+#pragma unroll
+                for (int s = 0; s < DV; ++s) dv[s] = d0;
+                h = (LR0 < 1.0);
+            }
         } else if (live) {
-            double pr[DV];
-            double p = LR[c];
+            if (MSA) {  // v2c_s = LLR + c_0 + ... (skipping c_s); L = LLR + all
 #pragma unroll
-            for (int s = 0; s < DV; ++s) { pr[s] = p; p = p * l[c][s]; }
-            if (__builtin_isnan(p)) p = 1.0;
-            h = (p <= 1.0);
-            if (post) post[pj] = p;
-            double acc = 1.0;
+                for (int s = 0; s < DV; ++s) {
+                    double sum = pv[c];
 #pragma unroll
-            for (int s = DV - 1; s >= 0; --s) {
-                double v = pr[s] * acc;
-                if (__builtin_isnan(v)) v = 1.0;
-                acc = acc * l[c][s];
-                dv[s] = 1.0 - 2.0 / (1.0 + v);
+                    for (int r = 0; r < DV; ++r)
+                        if (r != s) sum = sum + l[c][r];
+                    dv[s] = sum;
+                }
+                double L = pv[c];
+#pragma unroll
+                for (int s = 0; s < DV; ++s) L = L + l[c][s];
+                h = !(L > 0);
+                if (post) post[pj] = L;
+            } else {
+                double pr[DV];
+                double p = pv[c];
+#pragma unroll
+                for (int s = 0; s < DV; ++s) { pr[s] = p; p = p * l[c][s]; }
+                if (__builtin_isnan(p)) p = 1.0;
+                h = (p <= 1.0);
+                if (post) post[pj] = p;
+                double acc = 1.0;
+#pragma unroll
+                for (int s = DV - 1; s >= 0; --s) {
+                    double v = pr[s] * acc;
+                    if (__builtin_isnan(v)) v = 1.0;
+                    acc = acc * l[c][s];
+                    dv[s] = 1.0 - 2.0 / (1.0 + v);
+                }
             }
         }
         if (fr || live) {
 #pragma unroll
-            for (int s = 0; s < DV; ++s) st<NT>(dmsg + (tb + eid[c][s]) * TILE + lane, dv[s]);
+            for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
         }
         const uint64_t m = __ballot(h);
         if (lane == 0) {

@@ -250,9 +250,9 @@ def test_grouped_schedules_bitexact(gpu, og, codewords, monkeypatch, group, nt, 
 
 @pytest.mark.parametrize("cpw,cont", [(2, 0), (4, 1), (8, 0), (2, 1)])
 def test_variable_columns_per_wave_bitexact(gpu, og, codewords, monkeypatch, cpw, cont):
-    """k_var_bp_m (CPW columns per wave) changes only which wave handles a
-    column, never a column's arithmetic; with continuous batching its
-    refill path initialises fresh lanes."""
+    """k_var_m (CPW columns per wave, BP and min-sum) changes only which
+    wave handles a column, never a column's arithmetic; with continuous
+    batching its refill path initialises fresh lanes."""
     monkeypatch.setenv("LDPC_VAR_CPW", str(cpw))
     monkeypatch.setenv("LDPC_CONT", str(cont))
     G2 = gpu.Graph(PCHK)
@@ -260,6 +260,8 @@ def test_variable_columns_per_wave_bitexact(gpu, og, codewords, monkeypatch, cpw
     _cmp(G2, og, llr, 60)
     llr = synth.bsc_llrs(codewords, 0, 150, seed=7, p=0.004)
     _cmp(G2, og, llr, 40)
+    llr = synth.bsc_llrs(codewords, 0, 200, seed=8, p=0.002)
+    _cmp(G2, og, llr, 30, algo="msa")
 
 
 @pytest.mark.parametrize("chunk", [64, 128])
