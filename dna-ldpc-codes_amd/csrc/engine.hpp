@@ -42,6 +42,7 @@ struct Engine {
     bool pipe = false;        // check(g+1) on `stream` overlaps variable(g) on `stream2`
     bool lr_csc = false;      // c2v scratch in column (CSC) order (regular kernels only)
     bool cont = false;        // continuous batching: refill lanes as codewords finish
+    int full_lanes = 0;       // all lanes of an active tile store (whole cache lines)
     int var_cpw = 1;          // variable phase: columns per wave (k_var_m when > 1)
     static constexpr int kRing = 8, kLag = 2;
     uint64_t* d_fresh = nullptr;

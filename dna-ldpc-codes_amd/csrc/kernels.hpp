@@ -194,7 +194,7 @@ template <int DC, bool NT, bool CSCL>
 __global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ dmsg, double* __restrict__ lr,
                                                      const uint64_t* __restrict__ active,
                                                      const int32_t* __restrict__ pos, int32_t M, int64_t E,
-                                                     int64_t t0)
+                                                     int64_t t0, int full_lanes)
 {
     constexpr int SEG = 8;
     constexpr int NSEG = (DC + SEG - 1) / SEG;
@@ -203,7 +203,9 @@ __global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ 
     const int64_t t = t0 + blockIdx.y;
     if (row >= M) return;
     const uint64_t act = active[t];
-    if (!((act >> lane) & 1ull)) return;
+    // full_lanes: converged / empty lanes of an active tile run along on their
+    // stale state so every c2v store covers whole lines (their values are never read)
+    if (full_lanes ? act == 0 : !((act >> lane) & 1ull)) return;
     const double* __restrict__ src = dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
     // c2v scratch: CSR order (row-contiguous) or CSC order (column-contiguous,
     // position pos[e]) so the variable phase reads each column contiguously
@@ -359,7 +361,7 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
                                                double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                const uint64_t* __restrict__ active,
                                                const int32_t* __restrict__ col_edge, double* __restrict__ post,
-                                               int32_t N, int64_t E, int64_t t0, Refill rf)
+                                               int32_t N, int64_t E, int64_t t0, Refill rf, int full_lanes)
 {
     const int lane = lane_id();
     const int32_t j0 = (xcd_block(blockIdx.x, gridDim.x) * 4 + wave_id()) * CPW;
@@ -392,6 +394,8 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
         const size_t pj = ((size_t)t * N + j) * TILE + lane;
         bool h = false;
         double dv[DV];
+#pragma unroll
+        for (int s = 0; s < DV; ++s) dv[s] = 0.0;
         if (fr) {  // Init_Belief_Propagation / Init_MSA_INF for a refilled lane
             const double x = rf.in[(size_t)rf.lane_b[t * TILE + lane] * N + j];
             if (MSA) {
@@ -440,7 +444,7 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
                 }
             }
         }
-        if (fr || live) {
+        if (full_lanes || fr || live) {  // full_lanes: whole-line stores (others write 0, never read)
 #pragma unroll
             for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
         }
@@ -515,14 +519,16 @@ template <int DC, bool NT, bool CSCL>
 __global__ __launch_bounds__(256) void k_check_msa(const double* __restrict__ v2c, double* __restrict__ c2v,
                                                    const uint64_t* __restrict__ active,
                                                    const int32_t* __restrict__ pos, int32_t M, int64_t E,
-                                                   int64_t t0)
+                                                   int64_t t0, int full_lanes)
 {
     const int lane = lane_id();
     const int32_t row = blockIdx.x * 4 + wave_id();
     const int64_t t = t0 + blockIdx.y;
     if (row >= M) return;
     const uint64_t act = active[t];
-    if (!((act >> lane) & 1ull)) return;
+    // full_lanes: converged / empty lanes of an active tile run along on their
+    // stale state so every c2v store covers whole lines (their values are never read)
+    if (full_lanes ? act == 0 : !((act >> lane) & 1ull)) return;
     const double* __restrict__ src = v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
     double* __restrict__ dst = c2v + (size_t)blockIdx.y * E * TILE + lane;
     const int32_t* __restrict__ prow = pos + (size_t)row * DC;
