@@ -14,6 +14,8 @@ run() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$OUT/$name.o
 
 run bench_default 900 python bench.py
 run trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$R/bench.py" --cpu-baseline 0 "$@"
+# the per-dispatch trace (~190k rows) is too large to bring back; keep the stats
+rm -f "$OUT"/trace/*kernel_trace.csv
 run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" --cpu-baseline 0 --no-profile --steps 1 --warmup 0 --batch-per-gpu ${PMC_BATCH:-1024}
 run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 "$R/bench.py" --cpu-baseline 0 --no-profile --steps 1 --warmup 0 --batch-per-gpu ${PMC_BATCH:-1024}
 run pmc_dram 600 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum -d "$OUT/pmc_dram" -o run --output-format csv -- python3 "$R/bench.py" --cpu-baseline 0 --no-profile --steps 1 --warmup 0 --batch-per-gpu ${PMC_BATCH:-1024}
