@@ -379,7 +379,12 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
     for (int c = 0; c < CPW; ++c)
 #pragma unroll
         for (int s = 0; s < DV; ++s) eid[c][s] = col_edge[(size_t)(j0 + c) * DV + s];
-    double l[CPW][DV], pv[CPW];
+    double l[CPW][DV], pv[CPW], xin[CPW];
+    if (fr) {  // refilled lane: its input row, prefetched with the c2v loads
+        const double* __restrict__ in_row = rf.in + (size_t)rf.lane_b[t * TILE + lane] * N;
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) xin[c] = in_row[j0 + c];
+    }
     if (live) {
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
@@ -397,7 +402,7 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
 #pragma unroll
         for (int s = 0; s < DV; ++s) dv[s] = 0.0;
         if (fr) {  // Init_Belief_Propagation / Init_MSA_INF for a refilled lane
-            const double x = rf.in[(size_t)rf.lane_b[t * TILE + lane] * N + j];
+            const double x = xin[c];
             if (MSA) {
                 prior[pj] = x;
 #pragma unroll
