@@ -401,16 +401,18 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
         double dv[DV];
 #pragma unroll
         for (int s = 0; s < DV; ++s) dv[s] = 0.0;
+        double np = 0.0;  // the prior this lane holds after the step (refill: its new one)
+        if (live) np = pv[c];
         if (fr) {  // Init_Belief_Propagation / Init_MSA_INF for a refilled lane
             const double x = xin[c];
             if (MSA) {
-                prior[pj] = x;
+                np = x;
 #pragma unroll
                 for (int s = 0; s < DV; ++s) dv[s] = x;
                 h = !(x > 0);
             } else {
                 const double LR0 = rf.in_is_llr ? exp(x) : x;
-                prior[pj] = LR0;
+                np = LR0;
                 const double d0 = 1.0 - 2.0 / (1.0 + LR0);
 #pragma unroll
                 for (int s = 0; s < DV; ++s) dv[s] = d0;
@@ -449,6 +451,9 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
                 }
             }
         }
+        // refills: the whole wave stores the prior line (live lanes their own
+        // value) instead of a partial-line write by the refilled lanes alone
+        if (CONT && frm != 0ull && (full_lanes >= 2 || fr)) prior[pj] = np;
         if (full_lanes || fr || live) {  // full_lanes: whole-line stores (others write 0, never read)
 #pragma unroll
             for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
