@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ 
     const uint64_t act = active[t];
     // full_lanes: converged / empty lanes of an active tile run along on their
     // stale state so every c2v store covers whole lines (their values are never read)
-    if (full_lanes ? act == 0 : !((act >> lane) & 1ull)) return;
+    if ((full_lanes & 1) ? act == 0 : !((act >> lane) & 1ull)) return;
     const double* __restrict__ src = dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
     // c2v scratch: CSR order (row-contiguous) or CSC order (column-contiguous,
     // position pos[e]) so the variable phase reads each column contiguously
@@ -388,7 +388,9 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
     if (live) {
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
-            pv[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
+            // bit 1 of full_lanes: nontemporal prior loads (keep the c2v group resident)
+            pv[c] = (full_lanes & 2) ? ld<true>(prior + ((size_t)t * N + j0 + c) * TILE + lane)
+                                     : prior[((size_t)t * N + j0 + c) * TILE + lane];
 #pragma unroll
             for (int s = 0; s < DV; ++s) l[c][s] = c2v[(tl + (size_t)eid[c][s]) * TILE + lane];
         }
@@ -453,8 +455,8 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
         }
         // refills: the whole wave stores the prior line (live lanes their own
         // value) instead of a partial-line write by the refilled lanes alone
-        if (CONT && frm != 0ull && (full_lanes >= 2 || fr)) prior[pj] = np;
-        if (full_lanes || fr || live) {  // full_lanes: whole-line stores (others write 0, never read)
+        if (CONT && frm != 0ull && ((full_lanes & 4) || fr)) prior[pj] = np;
+        if ((full_lanes & 1) || fr || live) {  // whole-line stores (others write 0, never read)
 #pragma unroll
             for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
         }
@@ -538,7 +540,7 @@ __global__ __launch_bounds__(256) void k_check_msa(const double* __restrict__ v2
     const uint64_t act = active[t];
     // full_lanes: converged / empty lanes of an active tile run along on their
     // stale state so every c2v store covers whole lines (their values are never read)
-    if (full_lanes ? act == 0 : !((act >> lane) & 1ull)) return;
+    if ((full_lanes & 1) ? act == 0 : !((act >> lane) & 1ull)) return;
     const double* __restrict__ src = v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
     double* __restrict__ dst = c2v + (size_t)blockIdx.y * E * TILE + lane;
     const int32_t* __restrict__ prow = pos + (size_t)row * DC;
