@@ -100,6 +100,30 @@ def test_erasures_and_extreme_llrs(G, og, codewords):
     _cmp(G, og, llr, 30, algo="msa")
 
 
+def test_nan_and_infinite_llrs(G, og, codewords):
+    """NaN and +-inf channel LLRs: BP's LR = exp(x) becomes NaN / inf / 0 and
+    runs into the NaN -> 1 guards; min-sum's |v2c| NaN exercises the
+    reference's first-other-edge semantics.  Hard bits, iterations and valid
+    flags bit-exact; posteriors equal bit for bit except that any NaN only
+    has to be matched by a NaN (payload and sign of a NaN are not part of the
+    contract)."""
+    rng = np.random.default_rng(12)
+    llr = synth.bsc_llrs(codewords, 0, 64, seed=10, p=0.005)
+    llr[rng.random(llr.shape) < 0.002] = np.nan
+    llr[rng.random(llr.shape) < 0.002] = np.inf
+    llr[rng.random(llr.shape) < 0.002] = -np.inf
+    llr[:4] = np.nan  # whole codewords of NaN
+    for algo, a in (("bp", 0), ("msa", 1)):
+        ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 30, algo=a, post_mode=1 if a == 0 else 0, threads=8)
+        h, p, it, v = G.decode(llr, max_iter=30, algo=algo, post="ratio" if a == 0 else "llr")
+        assert np.array_equal(it, ref_it), algo
+        assert np.array_equal(v, ref_v.astype(bool)), algo
+        assert np.array_equal(h, ref_h), algo
+        nan = np.isnan(ref_p)
+        assert np.array_equal(np.isnan(p), nan), algo
+        assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64)), algo
+
+
 def test_multi_pass_chunking(G, og, codewords):
     """B larger than the resident chunk: passes of 64 codewords."""
     llr = synth.bsc_llrs(codewords, 0, 150, seed=4, p=0.006)
