@@ -108,12 +108,21 @@ def trial_from_reads(reads, codewords: np.ndarray, eps: float = 0.02, max_iter: 
     return res
 
 
-def report(res: Dict, rs: int = 72000) -> str:
-    """The o_/x_ result-file body (decoder.py:668-727) without the wall time."""
-    n = res["n"]
+def report(res: Dict, rs: int = 72000, total_time: Optional[float] = None, threshold: Optional[int] = None,
+           newline: str = "\n") -> str:
+    """The o_/x_ result-file body (decoder.py:668-727).  total_time adds the
+    'Total time: %f sec' line; threshold adds the 'Re-decoding threshold
+    (number): %d' line of the committed o_72000_7_*_result.txt files (written
+    by a revision of decoder.py that had it, on Windows: newline='\r\n')."""
     ok = not res["fail_second"]
     fmt = lambda xs: ("None" if not xs else " ".join(str(v) for v in xs) + " ")  # noqa: E731
-    lines = ["=" * 78, " " * 31 + "Results" + " " * 40, "=" * 78, f"Random Sampling Number: {rs}"]
+    n = res["n"]
+    lines = ["=" * 78, " " * 31 + "Results" + " " * 40, "=" * 78]
+    if total_time is not None:
+        lines.append("Total time: %f sec" % total_time)
+    lines.append(f"Random Sampling Number: {rs}")
+    if threshold is not None:
+        lines.append("Re-decoding threshold (number): %d" % threshold)
     if ok:
         lines += ["Decoding success", "", "First decoding result:   %d/%d" % (res["first_success"], n),
                   "Second decoding result:  %d/%d" % (res["second_success"], n),
@@ -123,4 +132,13 @@ def report(res: Dict, rs: int = 72000) -> str:
                   "Second decoding result:\t%d/%d" % (res["second_success"], n)]
     lines += ["First decoding failure index: " + fmt(res["fail_first"]),
               "Second decoding failure index: " + fmt(res["fail_second"])]
-    return "\n".join(lines) + "\n"
+    return newline.join(lines) + newline
+
+
+def result_file_name(res: Dict, rs: int, trial: int, eps: float, threshold: Optional[int] = None) -> str:
+    """o_/x_ file name of decoder.py:668-671; with threshold, the
+    o_<rs>_<threshold>_<trial>_<eps> form of the committed result files."""
+    head = "o" if not res["fail_second"] else "x"
+    if threshold is None:
+        return head + "_%d_%d_%f_result.txt" % (rs, trial, eps)
+    return head + "_%d_%d_%d_%f_result.txt" % (rs, threshold, trial, eps)
