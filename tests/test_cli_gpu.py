@@ -72,3 +72,40 @@ def test_cli_targeting_and_frames(tmp_path, codewords):
     res = os.path.join(d, f"result_({soft}.txt)_decode_n18432_m2048_final.pchk_0_0.000dB_0_5_7.txt")
     txt = open(res).read()
     assert "target_VN:1~100" in txt and "# of Frame[ 0]          :3" in txt
+
+
+def test_config1_plumbing_cli(tmp_path, og, codewords):
+    """B = 1, codeword_n18432_m1860_1, LLR +-ln 49 from
+    BSC p = 0.02 drawn with numpy default_rng(0), 50 BP iterations through the
+    file-compatible CLI; the decode fails after all 50 iterations, as in the
+    oracle."""
+    d = str(tmp_path)
+    rng = np.random.default_rng(0)
+    y = codewords[0] ^ (rng.random(codewords.shape[1]) < 0.02).astype(np.uint8)
+    llr = np.where(y == 1, -synth.LLR_UNIT, synth.LLR_UNIT)
+    cwb, soft = _write_inputs(d, codewords[0], llr)
+    argv = [EXE, "0", "0", "0", "7", "50", "1", cwb, soft, "decode_n18432_m2048_final", "0", "0", "0", "0"]
+    r = subprocess.run(argv, cwd=d, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    dec = np.array(open(os.path.join(d, f"dec_{cwb}.txt")).read().split(), dtype=np.uint8)
+    h, _, it, v = og.decode_batch(llr[None, :], 50, algo=0, threads=1, want_post=False)
+    assert it[0] == 50 and not v[0]
+    assert np.array_equal(dec, h[0])
+
+
+@pytest.mark.parametrize("dtype,algo", [(1, 3), (2, 4), (3, 5), (21, 1), (22, 1)])
+def test_cli_other_decoder_types(tmp_path, og, codewords, dtype, algo):
+    """decoder_type 1/2/3 -> Gallager A/B1/B2 on the soft input's hard
+    decision, 21/22 -> float min-sum (the DNA build's g_precision = 0)."""
+    d = str(tmp_path)
+    llr = synth.bsc_llrs(codewords, 0, 1, seed=99, p=0.002)[0]
+    cwb, soft = _write_inputs(d, codewords[0], llr)
+    argv = [EXE, "0", str(dtype), "0", "7", "30", "1", cwb, soft, "decode_n18432_m2048_final", "0", "0", "0", "0"]
+    r = subprocess.run(argv, cwd=d, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    dec = np.array(open(os.path.join(d, f"dec_{cwb}.txt")).read().split(), dtype=np.uint8)
+    if algo == 1:
+        h, _, _, _ = og.decode_batch(llr[None, :], 30, algo=1, threads=1, want_post=False)
+    else:
+        h, _, _, _ = og.decode_int_batch(llr[None, :], 30, algo)
+    assert np.array_equal(dec, h[0])
