@@ -218,12 +218,21 @@ def main():
 
     # ---- roofline of the dominant kernel (algorithmic bytes) ----
     cw_iters = float(iters.sum()) * args.steps  # executed codeword-iterations (this rank)
-    by_kernel = {
-        # check phase: read E v->c (d) + write E c->v (lr), fp64
-        "check": 16.0 * E,
-        # variable phase: read E lr + N LR, write E d + N/8 hard-bit ballots
-        "variable": 16.0 * E + 8.0 * N + N / 8.0,
-    }
+    M = G.M
+    if eng.msa_compressed:
+        # compressed min-sum c2v (MSA-C): the check phase
+        # reads E v->c fp64 and writes E code bytes + the (min1, min2) record
+        # planes (2 x 8 B per row; the NaN planes only when NaN occurs); the
+        # variable phase reads the codes, the records once, N LLR, writes E
+        # v->c fp64 + N/8 hard-bit ballots
+        by_kernel = {"check": 9.0 * E + 16.0 * M, "variable": 9.0 * E + 16.0 * M + 8.0 * N + N / 8.0}
+    else:
+        by_kernel = {
+            # check phase: read E v->c (d) + write E c->v (lr), fp64
+            "check": 16.0 * E,
+            # variable phase: read E lr + N LR, write E d + N/8 hard-bit ballots
+            "variable": 16.0 * E + 8.0 * N + N / 8.0,
+        }
     def avg_ms(k):
         return st[k]["ms"] / st[k]["sampled"] if st[k]["sampled"] else 0.0
 
@@ -236,7 +245,7 @@ def main():
     iter_bytes = (32.0 * E + 10.0 * N) * cw_iters
     # traffic: HBM bytes per codeword-iteration of this kernel from the committed
     # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE), scaled to this launch size
-    kname = f"k_{'check' if dom == 'check' else 'var'}_{algo}"
+    kname = f"k_{'check' if dom == 'check' else 'var'}_{algo}" + ("_c" if eng.msa_compressed else "")
     traffic, traffic_src = None, None
     for tf in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
         tj = json.load(open(tf))

@@ -368,7 +368,8 @@ int ldpc_engine_info(ldpc_engine* e, int64_t* cap, int64_t* group_tiles, int32_t
     if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
     if (cap) *cap = e->e->cap;
     if (group_tiles) *group_tiles = e->e->group_tiles;
-    if (flags) *flags = (e->e->nt_d ? 1 : 0) | (e->e->pipe ? 2 : 0) | (e->e->lr_csc ? 4 : 0) | (e->e->cont ? 8 : 0);
+    if (flags) *flags = (e->e->nt_d ? 1 : 0) | (e->e->pipe ? 2 : 0) | (e->e->lr_csc ? 4 : 0) | (e->e->cont ? 8 : 0) |
+                        (e->e->msa_c ? 16 : 0);
     return LDPC_OK;
 }
 

@@ -38,6 +38,9 @@ constexpr int64_t kDefaultCsc = 0;
 constexpr int64_t kDefaultCont = 1;
 constexpr int64_t kDefaultC2vProbe = 4;  // LDPC_C2V_PROBE: candidate c2v scratch buffers timed at init
 constexpr int64_t kDefaultFullLanes = 1;  // LDPC_FULL_LANES: whole-wave stores in partially converged tiles (A/B: MSA p=.002 +5.6%, BP p=.002 +7.5%, config 3 neutral)
+constexpr int64_t kDefaultMsaGroupTiles = 4;  // LDPC_GROUP_TILES default for compressed min-sum (A/B, 1024-lane pool)
+constexpr int64_t kDefaultMsaPool = 1024;  // LDPC_MSA_POOL: resident lanes, compressed min-sum + continuous mode (A/B)
+constexpr int64_t kDefaultMsaC = 1;  // LDPC_MSA_C: compressed min-sum c2v (tools/icbench: 52.6 -> 33.5 us per tile-iteration)
 constexpr int64_t kDefaultVarCpw = 4;  // LDPC_VAR_CPW (A/B over two boxes: +2.6-2.9% over 1 column per wave)
 
 static thread_local std::string g_err;
@@ -68,7 +71,7 @@ Engine::~Engine()
     if (h_occ) hipHostFree(h_occ);
     for (int i = 0; i < kRing; i++)
         if (ev_ring[i]) hipEventDestroy(ev_ring[i]);
-    hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge);
+    hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge); hipFree(d_col_row);
     hipFree(v2c); hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
     hipFree(post_t);
     if (stream) hipStreamDestroy(stream);
@@ -104,11 +107,19 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     LDPC_HIP(hipSetDevice(dev));
     LDPC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
 
+    if (nt < 0) nt = (int)env_int("LDPC_NT_D", kDefaultNT);
+    const bool reg_72_8 = g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
+    msa_c = algo == LDPC_ALGO_MSA && reg_72_8 && nt != 0 && g->N % 16 == 0 && env_int("LDPC_MSA_C", kDefaultMsaC) != 0;
+    if (cont_mode < 0) cont_mode = (int)env_int("LDPC_CONT", kDefaultCont);
+    cont = cont_mode != 0 && !int_algo && reg_72_8;
     if (chunk <= 0) {
         size_t fr = 0, tot = 0;
         LDPC_HIP(hipMemGetInfo(&fr, &tot));
-        // half of the free memory for the resident state, at most 16384 codewords
-        chunk = std::min<int64_t>(16384, (int64_t)(fr / 2) / engine_bytes_per_codeword(*g));
+        // half of the free memory for the resident state, at most 16384 codewords;
+        // compressed min-sum in continuous mode: a small lane pool (its scattered
+        // v2c stores run ~45 % longer over a 19 GB pool than over 1.2 GB, A/B)
+        const int64_t want = (msa_c && cont) ? env_int("LDPC_MSA_POOL", kDefaultMsaPool) : 16384;
+        chunk = std::min<int64_t>(want, (int64_t)(fr / 2) / engine_bytes_per_codeword(*g));
     }
     cap = std::max<int64_t>(64, (chunk + 63) / 64 * 64);
     cap_tiles = cap / 64;
@@ -116,8 +127,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     // group: tiles whose check->variable messages are live at once.  Small
     // groups keep c2v resident in the 256 MB Infinity Cache between the check
     // and the variable phase; 0 = the whole pass.
-    if (group < 0) group = env_int("LDPC_GROUP_TILES", kDefaultGroupTiles);
-    if (nt < 0) nt = (int)env_int("LDPC_NT_D", kDefaultNT);
+    if (group < 0) group = env_int("LDPC_GROUP_TILES", msa_c ? kDefaultMsaGroupTiles : kDefaultGroupTiles);
     group_tiles = (group <= 0 || group > cap_tiles) ? cap_tiles : group;
     nt_d = nt != 0;
     if (pipelined < 0) pipelined = (int)env_int("LDPC_PIPE", kDefaultPipe);
@@ -135,6 +145,11 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     if ((rc = upload(&d_row_ptr, g->row_ptr)) || (rc = upload(&d_col_idx, g->col_idx)) ||
         (rc = upload(&d_col_ptr, g->col_ptr)) || (rc = upload(&d_col_edge, g->col_edge)))
         return rc;
+    if (msa_c) {
+        std::vector<int32_t> cr(g->col_edge.size());
+        for (size_t q = 0; q < cr.size(); q++) cr[q] = g->edge_row[(size_t)g->col_edge[q]];
+        if ((rc = upload(&d_col_row, cr))) return rc;
+    }
     if (g->regular_dc && g->dc_max > 0) {
         std::vector<int32_t> T((size_t)g->dc_max * g->M);
         for (int32_t i = 0; i < g->M; i++)
@@ -149,8 +164,6 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     var_cpw = (int)env_int("LDPC_VAR_CPW", kDefaultVarCpw);
     full_lanes = (int)env_int("LDPC_FULL_LANES", kDefaultFullLanes);
     if (var_cpw != 1 && var_cpw != 2 && var_cpw != 4 && var_cpw != 8) var_cpw = 1;
-    if (cont_mode < 0) cont_mode = (int)env_int("LDPC_CONT", kDefaultCont);
-    cont = cont_mode != 0 && !int_algo && g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
     if (cont) {
         LDPC_HIP(hipMalloc((void**)&d_fresh, (size_t)cap_tiles * sizeof(uint64_t)));
         LDPC_HIP(hipMalloc((void**)&d_occ, (size_t)cap_tiles * sizeof(uint64_t)));
@@ -356,6 +369,30 @@ static void var_regular(int algo, hipStream_t s, dim3 grid, const double* scratc
     else var_regular3<NT, CSCL, false>(algo, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
 }
 
+// MSA-C scratch: codes [c2v_tiles][E][64] u8, then records [c2v_tiles][M][4][64]
+// fp64, inside the c2v allocation (13.6 MB of its 75.5 MB per tile for the
+// DNA code; also with the two-slot `pipe` layout).
+static uint8_t* msa_codes(double* scratch) { return reinterpret_cast<uint8_t*>(scratch); }
+static double* msa_rec(double* scratch, int64_t tiles, int64_t E)
+{
+    return reinterpret_cast<double*>(reinterpret_cast<uint8_t*>(scratch) + (size_t)tiles * E * 64);
+}
+
+template <int CPW>
+static void var_msa_c(hipStream_t s, unsigned nb, const uint8_t* codes, const double* rec, double* v2c, double* prior,
+                      uint64_t* hard, const uint64_t* active, const int32_t* col_edge, const int32_t* col_row,
+                      double* pt, int32_t N, int32_t M, int64_t E, int64_t t0, unsigned gt, const dev::Refill& rf,
+                      int full)
+{
+    using namespace dev;
+    if (rf.fresh)
+        hipLaunchKernelGGL((k_var_msa_c<8, true, true, CPW>), dim3(nb), dim3(256), 0, s, codes, rec, v2c, prior, hard,
+                           active, col_edge, col_row, pt, N, M, E, t0, (uint32_t)gt, rf, full);
+    else
+        hipLaunchKernelGGL((k_var_msa_c<8, true, false, CPW>), dim3(nb), dim3(256), 0, s, codes, rec, v2c, prior, hard,
+                           active, col_edge, col_row, pt, N, M, E, t0, (uint32_t)gt, rf, full);
+}
+
 int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt)
 {
     using namespace dev;
@@ -363,6 +400,11 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
     const int64_t E = g->E;
     const bool reg72 = g->regular_dc && g->dc_max == 72;
     const dim3 grid((M + 3) / 4, gt), blk(256);
+    if (msa_c) {
+        LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa_c<72, true>), grid, blk, 0, s, v2c, msa_codes(scratch),
+                                                 msa_rec(scratch, c2v_tiles, E), active, M, E, t0, full_lanes));
+        return LDPC_OK;
+    }
     if (reg72) {
         LAUNCH_ON(s, K_CHECK, {
             if (nt_d && lr_csc) check_regular<true, true>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0, full_lanes);
@@ -386,6 +428,18 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
     const int64_t E = g->E;
     const bool reg8 = g->regular_dv && g->dv_max == 8;
     const dim3 grid((N + 3) / 4, gt), blk(256);
+    if (msa_c) {  // N % 16 == 0 (init)
+        const int cpw = var_cpw >= 4 ? 4 : var_cpw;
+        const unsigned nb = gt * (unsigned)(N / (4 * cpw));
+        const uint8_t* codes = msa_codes(scratch);
+        const double* rec = msa_rec(scratch, c2v_tiles, E);
+        LAUNCH_ON(s, K_VAR, {
+            if (cpw == 1) var_msa_c<1>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
+            else if (cpw == 2) var_msa_c<2>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
+            else var_msa_c<4>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
+        });
+        return LDPC_OK;
+    }
     if (reg8 && var_cpw > 1 && nt_d && !lr_csc && N % (4 * var_cpw) == 0) {
         const dim3 gm((unsigned)(N / (4 * var_cpw)), gt);
         LAUNCH_ON(s, K_VAR, var_multi(algo, var_cpw, s, gm, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf, full_lanes));

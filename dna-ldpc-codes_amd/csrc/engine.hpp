@@ -44,6 +44,7 @@ struct Engine {
     bool cont = false;        // continuous batching: refill lanes as codewords finish
     int full_lanes = 0;       // all lanes of an active tile store (whole cache lines)
     int var_cpw = 1;          // variable phase: columns per wave (k_var_m when > 1)
+    bool msa_c = false;       // min-sum with compressed c2v (records + codes, k_check_msa_c / k_var_msa_c)
     static constexpr int kRing = 8, kLag = 2;
     uint64_t* d_fresh = nullptr;
     uint64_t* d_occ = nullptr;
@@ -61,6 +62,7 @@ struct Engine {
     int32_t* d_col_idx_T = nullptr;  // [dc][M] for regular rows (syndrome gathers)
     int32_t* d_col_ptr = nullptr;
     int32_t* d_col_edge = nullptr;
+    int32_t* d_col_row = nullptr;  // [E] row of edge col_edge[q] (MSA-C record lookups)
     // decoder state
     double* v2c = nullptr;
     double* c2v = nullptr;

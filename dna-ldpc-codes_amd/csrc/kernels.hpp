@@ -725,6 +725,217 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// Compressed min-sum check->variable messages ("MSA-C", regular graphs).
+// A row's 72 outgoing messages take only four magnitudes -- min1, min2 and,
+// in the NaN cases derived above k_check_msa, |x_0| or |x_1| -- and a sign, so
+// the check phase writes per (row, lane) a record of those magnitudes and per
+// edge one code byte instead of 72 fp64 messages:
+//   rec   [group tile][M][4][64] fp64   planes m1, m2, n0 = |x_0|, n1 = |x_1|
+//                                       (n0 / n1 written only when NaN)
+//   codes [group tile][E][64] u8        bit 0: sign -1; bits 1-2: source plane
+// The variable phase rebuilds c2v = (double)sign * plane[source] -- the value
+// k_check_msa stores, by the same expression -- so every downstream sum is
+// unchanged.  Per edge and codeword the c2v stream shrinks from 16 B (write +
+// read) to 2 B plus the record (1 KB per row and wave, read 72 times while
+// resident in the XCD's L2; see k_var_msa_c for the XCD-affine tile order).
+// ---------------------------------------------------------------------------
+constexpr int MSA_REC_PLANES = 4;
+
+template <int DC, bool NT>
+__global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, uint8_t* __restrict__ codes,
+                                                     double* __restrict__ rec, const uint64_t* __restrict__ active,
+                                                     int32_t M, int64_t E, int64_t t0, int full_lanes)
+{
+    static_assert(DC >= 2 && DC <= 96, "row degree");
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = t0 + blockIdx.y;
+    if (row >= M) return;
+    const uint64_t act = active[t];
+    if ((full_lanes & 1) ? act == 0 : !((act >> lane) & 1ull)) return;
+    const double* __restrict__ src = v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
+    double x[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
+    // one pass: min1 with its FIRST index, min2 = minimum over the other
+    // indices (a tie with min1 gives min2 == min1), NaN never compares less
+    double m1 = __builtin_inf(), m2 = __builtin_inf();
+    int i1 = -1;
+    uint32_t negb[(DC + 31) / 32] = {};
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const double a = __builtin_fabs(x[k]);
+        negb[k / 32] |= ((x[k] >= 0) ? 0u : 1u) << (k % 32);
+        if (a < m1) { m2 = m1; m1 = a; i1 = k; }
+        else if (a < m2) m2 = a;
+    }
+    uint32_t neg = 0;
+#pragma unroll
+    for (int w = 0; w < (DC + 31) / 32; ++w) neg ^= (uint32_t)__builtin_popcount(negb[w]);
+    neg &= 1u;
+    const double a0 = __builtin_fabs(x[0]), a1 = __builtin_fabs(x[1]);
+    const bool nan0 = __builtin_isnan(a0), nan1 = __builtin_isnan(a1);
+    double* __restrict__ r = rec + ((size_t)blockIdx.y * M + row) * (MSA_REC_PLANES * TILE) + lane;
+    r[0] = m1;
+    r[TILE] = m2;
+    if (nan0) r[2 * TILE] = a0;
+    if (nan1) r[3 * TILE] = a1;
+    uint8_t* __restrict__ c = codes + ((size_t)blockIdx.y * E + (size_t)row * DC) * TILE + lane;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const uint32_t nk = (negb[k / 32] >> (k % 32)) & 1u;
+        const bool nanf = (k == 0) ? nan1 : nan0;
+        const uint32_t srcp = nanf ? (k == 0 ? 3u : 2u) : (k == i1 ? 1u : 0u);
+        c[(size_t)k * TILE] = (uint8_t)((neg ^ nk) | (srcp << 1));
+    }
+}
+
+// Min-sum variable phase on compressed messages (arithmetic of k_var_m<MSA>).
+// 1-D grid of gt * (N / (4 CPW)) blocks; block L works on group tile L % gt.
+// Workgroups are dispatched to the 8 XCDs round-robin, so when gt divides 8
+// every XCD only ever touches the records of one tile (2 MB), which stay in
+// its 4 MB L2 while they are re-read by the tile's 72 columns per row.
+template <int DV, bool NT, bool CONT, int CPW, bool SEL2 = false>
+__global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ codes, const double* __restrict__ rec,
+                                                   double* __restrict__ v2c, double* __restrict__ prior,
+                                                   uint64_t* __restrict__ hard, const uint64_t* __restrict__ active,
+                                                   const int32_t* __restrict__ col_edge,
+                                                   const int32_t* __restrict__ col_row, double* __restrict__ post,
+                                                   int32_t N, int32_t M, int64_t E, int64_t t0, uint32_t gt, Refill rf,
+                                                   int full_lanes)
+{
+    const int lane = lane_id();
+    const uint32_t ty = blockIdx.x % gt;
+    const int32_t j0 = (int32_t)((blockIdx.x / gt) * 4 + wave_id()) * CPW;
+    const int64_t t = t0 + ty;
+    if (j0 >= N) return;
+    const uint64_t act = active[t];
+    const uint64_t frm = CONT ? rf.fresh[t] : 0ull;
+    const uint64_t touched = act | frm;
+    if (touched == 0) return;
+    const bool live = (act >> lane) & 1ull;
+    const bool fr = CONT && ((frm >> lane) & 1ull);
+    const size_t tb = (size_t)t * E;
+    int32_t eid[CPW][DV], rid[CPW][DV];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c)
+#pragma unroll
+        for (int s = 0; s < DV; ++s) {
+            eid[c][s] = col_edge[(size_t)(j0 + c) * DV + s];
+            rid[c][s] = col_row[(size_t)(j0 + c) * DV + s];
+        }
+    const uint8_t* __restrict__ cg = codes + (size_t)ty * E * TILE + lane;
+    const double* __restrict__ rg = rec + (size_t)ty * M * (MSA_REC_PLANES * TILE) + lane;
+    double l[CPW][DV], pv[CPW], xin[CPW];
+    if (fr) {
+        const double* __restrict__ in_row = rf.in + (size_t)rf.lane_b[t * TILE + lane] * N;
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) xin[c] = in_row[j0 + c];
+    }
+    if (live) {
+        uint32_t cd[CPW][DV];
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) {
+            pv[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
+#pragma unroll
+            for (int s = 0; s < DV; ++s) cd[c][s] = cg[(size_t)eid[c][s] * TILE];
+        }
+        if constexpr (SEL2) {
+            // min1 and min2 planes both loaded (whole 512-B segments, no
+            // dependence on the code); the NaN planes only when a lane needs one
+            double ma[CPW][DV], mb[CPW][DV];
+            uint32_t nanm = 0;
+#pragma unroll
+            for (int c = 0; c < CPW; ++c)
+#pragma unroll
+                for (int s = 0; s < DV; ++s) {
+                    const double* rr = rg + (size_t)rid[c][s] * (MSA_REC_PLANES * TILE);
+                    ma[c][s] = rr[0];
+                    mb[c][s] = rr[TILE];
+                }
+#pragma unroll
+            for (int c = 0; c < CPW; ++c)
+#pragma unroll
+                for (int s = 0; s < DV; ++s) {
+                    const uint32_t sp = (cd[c][s] >> 1) & 3u;
+                    l[c][s] = (sp & 1u) ? mb[c][s] : ma[c][s];
+                    nanm |= sp >> 1;
+                }
+            if (__builtin_expect(nanm != 0, 0)) {
+#pragma unroll
+                for (int c = 0; c < CPW; ++c)
+#pragma unroll
+                    for (int s = 0; s < DV; ++s) {
+                        const uint32_t sp = (cd[c][s] >> 1) & 3u;
+                        const size_t o = ((size_t)rid[c][s] * MSA_REC_PLANES + (sp | 2u)) * TILE;
+                        const double nv = rg[o];  // harmless extra read for lanes that do not use it
+                        if (sp >= 2) l[c][s] = nv;
+                    }
+            }
+        } else {
+            // one record load per edge, from the plane the code names
+#pragma unroll
+            for (int c = 0; c < CPW; ++c)
+#pragma unroll
+                for (int s = 0; s < DV; ++s) {
+                    const uint32_t sp = (cd[c][s] >> 1) & 3u;
+                    l[c][s] = rg[((size_t)rid[c][s] * MSA_REC_PLANES + sp) * TILE];
+                }
+        }
+#pragma unroll
+        for (int c = 0; c < CPW; ++c)
+#pragma unroll
+            for (int s = 0; s < DV; ++s) {
+                const int sign = (cd[c][s] & 1u) ? -1 : 1;
+                l[c][s] = (double)sign * l[c][s];
+            }
+    }
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        const int32_t j = j0 + c;
+        const size_t pj = ((size_t)t * N + j) * TILE + lane;
+        bool h = false;
+        double dv[DV];
+#pragma unroll
+        for (int s = 0; s < DV; ++s) dv[s] = 0.0;
+        double np = 0.0;
+        if (live) np = pv[c];
+        if (fr) {  // Init_MSA_INF for a refilled lane
+            const double x = xin[c];
+            np = x;
+#pragma unroll
+            for (int s = 0; s < DV; ++s) dv[s] = x;
+            h = !(x > 0);
+        } else if (live) {  // v2c_s = LLR + c_0 + ... (skipping c_s); L = LLR + all
+#pragma unroll
+            for (int s = 0; s < DV; ++s) {
+                double sum = pv[c];
+#pragma unroll
+                for (int q = 0; q < DV; ++q)
+                    if (q != s) sum = sum + l[c][q];
+                dv[s] = sum;
+            }
+            double L = pv[c];
+#pragma unroll
+            for (int s = 0; s < DV; ++s) L = L + l[c][s];
+            h = !(L > 0);
+            if (post) post[pj] = L;
+        }
+        if (CONT && frm != 0ull && ((full_lanes & 4) || fr)) prior[pj] = np;
+        if ((full_lanes & 1) || fr || live) {
+#pragma unroll
+            for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
+        }
+        const uint64_t m = __ballot(h);
+        if (lane == 0) {
+            const size_t o = (size_t)t * N + j;
+            const uint64_t old = (touched == ~0ull) ? 0ull : hard[o];
+            hard[o] = (old & ~touched) | (m & touched);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // finalize: posterior per codeword/bit, written row-major [b][N].  The
 // variable phase leaves the posterior of its iteration in post_t ([t][N][64]):
 //   BP : P = LR * prod lr (ascending row, dec.cpp:669-674), NaN -> 1

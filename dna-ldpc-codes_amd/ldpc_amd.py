@@ -426,6 +426,7 @@ class Engine:
         self.cap, self.group_tiles = cap.value, grp.value
         self.nontemporal, self.pipeline, self.csc_scratch = bool(fl.value & 1), bool(fl.value & 2), bool(fl.value & 4)
         self.continuous = bool(fl.value & 8)
+        self.msa_compressed = bool(fl.value & 16)  # min-sum c2v as per-row records + per-edge codes
 
     def decode(self, d_in, in_kind: int, B: int, max_iter: int, d_hard=None, d_post=None, post_kind=POST_LLR,
                d_iters=None, d_valid=None):

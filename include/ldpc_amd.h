@@ -204,12 +204,14 @@ typedef struct ldpc_kernel_stats {
 
 int ldpc_engine_profile(ldpc_engine *e, int32_t stride);
 
-/* The schedule an engine runs with: group tiles, nontemporal flag, resident
- * codewords per pass. */
 /* Parameters of LDPC_ALGO_QMSA (ignored by the other algorithms); the
  * engine starts with q = 6, step = 0.5, beta = 0, seed = 0. */
 int ldpc_engine_set_params(ldpc_engine *e, int32_t msa_precision, double msa_step, int32_t msa_offset,
                            uint64_t tie_seed);
+/* The schedule an engine runs with: resident codewords per pass (the lane
+ * pool in continuous mode), group tiles, and flags with the bits of
+ * ldpc_engine_create_ex plus bit 4 = compressed min-sum check->variable
+ * messages (env LDPC_MSA_C). */
 int ldpc_engine_info(ldpc_engine *e, int64_t *cap, int64_t *group_tiles, int32_t *flags);
 int ldpc_engine_stats(ldpc_engine *e, ldpc_kernel_stats *out);
 

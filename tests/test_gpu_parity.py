@@ -300,3 +300,36 @@ def test_continuous_batching_edge_cases(gpu, og, codewords, monkeypatch, chunk):
     _cmp(G2, og, llr, 25, chunk=chunk)
     _cmp(G2, og, llr[:70], 0, chunk=chunk)
     _cmp(G2, og, llr[:130], 12, algo="msa", chunk=chunk)
+
+
+@pytest.mark.parametrize("msa_c,group,cont,cpw", [(0, 3, 1, 4), (1, 1, 0, 1), (1, 2, 1, 2), (1, 3, 0, 4), (1, 8, 1, 4),
+                                                  (1, 0, 0, 2), (1, 2, 1, 8)])
+def test_min_sum_compressed_messages_bitexact(gpu, og, codewords, monkeypatch, msa_c, group, cont, cpw):
+    """MSA-C (kernels.hpp k_check_msa_c / k_var_msa_c): the check phase stores
+    per row the four magnitudes min1 / min2 / |x_0| / |x_1| and per edge a sign +
+    source code; the variable phase rebuilds each c2v by the reference's
+    expression, so hard bits, iterations, valid flags and the posterior L stay
+    bit-exact -- across group sizes (XCD-affine tile order), continuous
+    batching, columns per wave, and the NaN / inf first-other-edge cases."""
+    monkeypatch.setenv("LDPC_MSA_C", str(msa_c))
+    monkeypatch.setenv("LDPC_GROUP_TILES", str(group))
+    monkeypatch.setenv("LDPC_CONT", str(cont))
+    monkeypatch.setenv("LDPC_VAR_CPW", str(cpw))
+    G2 = gpu.Graph(PCHK)
+    llr = synth.bsc_llrs(codewords, 0, 300, seed=2026, p=0.002)
+    _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa")
+    assert len(np.unique(it)) > 2
+    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 70, seed=5, p=0.01), 12, algo="msa")
+    rng = np.random.default_rng(13)
+    llr = synth.bsc_llrs(codewords, 0, 130, seed=11, p=0.004)
+    llr[rng.random(llr.shape) < 0.003] = np.nan
+    llr[rng.random(llr.shape) < 0.002] = np.inf
+    llr[rng.random(llr.shape) < 0.002] = -np.inf
+    llr[rng.random(llr.shape) < 0.01] = -0.0
+    llr[:2] = np.nan
+    ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 20, algo=1, post_mode=0, threads=8)
+    h, p, it, v = G2.decode(llr, max_iter=20, algo="msa", post="llr")
+    assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
+    nan = np.isnan(ref_p)
+    assert np.array_equal(np.isnan(p), nan)
+    assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64))

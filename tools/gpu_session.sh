@@ -13,7 +13,7 @@ cd "$R"
 export TMPDIR=/tmp
 fatal() { local rc=$1; [ "$rc" -ge 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 139 ]; }
 
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest gpu rc=$rc"; tail -5 "$OUT/pytest_gpu.log"
 if fatal $rc; then echo "fatal after pytest"; exit $rc; fi
 

@@ -1,0 +1,256 @@
+// icbench.hip -- schedule micro-benchmark (not part of the product): the real
+// BP check / variable kernels of csrc/kernels.hpp on the DNA graph, timed per
+// 64-codeword tile-iteration under two schedules:
+//
+//   stream  : the engine's current schedule -- d ("v2c") for P tiles in HBM,
+//             c2v scratch for one group of G tiles, per iteration
+//             check(g) -> scratch, variable(g) -> d for every group
+//   resident: messages in place (one E x 64 buffer per tile: the check phase
+//             overwrites d with lr, the variable phase lr with d), a group of
+//             T tiles iterated back to back so its whole state
+//             (T x (75.5 + 9.4) MB) can stay in the 256 MB Infinity Cache
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//       -I dna-ldpc-codes_amd/csrc -o tools/icbench tools/icbench.hip dna-ldpc-codes_amd/csrc/graph.cpp
+//   tools/icbench tests/golden/decode_n18432_m2048_final.pchk
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "graph.hpp"
+#include "kernels.hpp"
+
+#define CK(x)                                                                                    \
+    do {                                                                                         \
+        hipError_t e = (x);                                                                      \
+        if (e != hipSuccess) { std::printf("%s: %s\n", #x, hipGetErrorString(e)); std::exit(1); } \
+    } while (0)
+
+using namespace ldpc;
+using namespace ldpc::dev;
+
+template <typename T>
+static T* up(const std::vector<T>& v)
+{
+    T* p;
+    CK(hipMalloc(&p, v.size() * sizeof(T)));
+    CK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return p;
+}
+
+__global__ void k_rand(double* p, size_t n)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t h = splitmix64(i);
+        const double u = (double)(h >> 11) * 0x1.0p-53;
+        p[i] = (h & 1) ? -(0.05 + 0.9 * u) : (0.05 + 0.9 * u);
+    }
+}
+
+__global__ void k_fill(double* p, size_t n, double v)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+int main(int argc, char** argv)
+{
+    if (argc < 2) { std::printf("usage: icbench file.pchk\n"); return 1; }
+    HostGraph g;
+    std::string msg;
+    if (load_pchk(argv[1], g, &msg)) { std::printf("load: %s\n", msg.c_str()); return 1; }
+    const int32_t M = g.M, N = g.N;
+    const int64_t E = g.E;
+    int32_t* d_col_edge = up(g.col_edge);
+    std::vector<int32_t> pos(E);
+    for (int64_t i = 0; i < E; i++) pos[i] = (int32_t)i;
+    int32_t* d_pos = up(pos);
+    const int P = argc > 2 ? std::atoi(argv[2]) : 24;  // tiles of the streamed d array (24: 1.8 GB)
+    const size_t tileE = (size_t)E * 64, tileN = (size_t)N * 64;
+    double *d, *scr, *prior;
+    CK(hipMalloc(&d, P * tileE * 8));
+    CK(hipMalloc(&scr, 4 * tileE * 8));
+    CK(hipMalloc(&prior, P * tileN * 8));
+    uint64_t *hard, *active;
+    CK(hipMalloc(&hard, (size_t)P * N * 8));
+    CK(hipMalloc(&active, P * 8));
+    std::vector<uint64_t> ones(P, ~0ull);
+    CK(hipMemcpy(active, ones.data(), P * 8, hipMemcpyHostToDevice));
+    // LR = 49 or 1/49 pattern, d = 1 - 2/(1+LR): values stay finite for the run
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, prior, P * tileN, 49.0);
+    hipLaunchKernelGGL(k_rand, dim3(4096), dim3(256), 0, 0, d, P * tileE);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const dim3 blk(256);
+    const Refill rf{};
+    auto check = [&](const double* src, double* dst, int64_t t0, unsigned gt, bool nt) {
+        if (nt) hipLaunchKernelGGL((k_check_bp<72, true, false>), dim3(M / 4, gt), blk, 0, 0, src, dst, active, d_pos, M, E, t0, 1);
+        else hipLaunchKernelGGL((k_check_bp<72, false, false>), dim3(M / 4, gt), blk, 0, 0, src, dst, active, d_pos, M, E, t0, 1);
+    };
+    auto var = [&](const double* src, double* dst, int64_t t0, unsigned gt, bool nt) {
+        if (nt) hipLaunchKernelGGL((k_var_m<false, 8, true, false, 4>), dim3(N / 16, gt), blk, 0, 0, src, dst, prior, hard, active, d_col_edge, (double*)nullptr, N, E, t0, rf, 1);
+        else hipLaunchKernelGGL((k_var_m<false, 8, false, false, 4>), dim3(N / 16, gt), blk, 0, 0, src, dst, prior, hard, active, d_col_edge, (double*)nullptr, N, E, t0, rf, 1);
+    };
+    const double algo_bytes = (32.0 * E + 10.0 * N) * 64;  // per tile-iteration
+    auto report = [&](const char* name, float ms, double tile_iters) {
+        const double us = ms * 1e3 / tile_iters;
+        std::printf("%-44s %8.2f us/tile-iter  %6.2f TB/s algorithmic  %7.0f cw/s @50it\n", name, us,
+                    algo_bytes / (us * 1e-6) / 1e12, 64.0 / (us * 1e-6) / 50.0);
+    };
+    // stream schedule, groups of G over P tiles
+    for (int G : {3}) {
+        for (int nt : {1, 0}) {
+            const int iters = 4;
+            for (int rep = 0; rep < 2; rep++) {
+                CK(hipEventRecord(e0));
+                for (int it = 0; it < iters; it++)
+                    for (int t0 = 0; t0 < P; t0 += G) {
+                        check(d, scr, t0, G, nt);
+                        var(scr, d, t0, G, nt);
+                    }
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+            }
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            char nm[64];
+            std::snprintf(nm, sizeof nm, "stream G=%d nt=%d (P=%d)", G, nt, P);
+            report(nm, ms, (double)iters * P);
+        }
+    }
+    // resident schedule: T tiles in place, all iterations back to back; the
+    // groups of tiles are visited one after another (each group's state is
+    // re-read from HBM once per visit)
+    for (int T : {1, 2, 3}) {
+        for (int nt : {0, 1}) {
+            for (int iters : {10, 50}) {
+                for (int rep = 0; rep < 2; rep++) {
+                    CK(hipEventRecord(e0));
+                    for (int t0 = 0; t0 + T <= 6; t0 += T)
+                        for (int it = 0; it < iters; it++) {
+                            // in place: the group's messages live in d[t0 .. t0+T)
+                            check(d, d + (size_t)t0 * tileE, t0, T, nt);
+                            var(d + (size_t)t0 * tileE, d, t0, T, nt);
+                        }
+                    CK(hipEventRecord(e1));
+                    CK(hipEventSynchronize(e1));
+                }
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                char nm[64];
+                std::snprintf(nm, sizeof nm, "resident T=%d nt=%d iters=%d", T, nt, iters);
+                report(nm, ms, (double)iters * (6 / T) * T);
+            }
+        }
+    }
+    // min-sum: full fp64 c2v (k_check_msa + k_var_m<MSA>) vs compressed
+    // records + codes (k_check_msa_c + k_var_msa_c), stream schedule
+    {
+        std::vector<int32_t> crow(g.col_edge.size());
+        for (size_t q = 0; q < crow.size(); q++) crow[q] = g.edge_row[g.col_edge[q]];
+        int32_t* d_col_row = up(crow);
+        const int iters = 4;
+        auto timeit = [&](auto&& body) {
+            float ms = 0;
+            for (int rep = 0; rep < 2; rep++) {
+                CK(hipEventRecord(e0));
+                for (int it = 0; it < iters; it++) body();
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+            }
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            return ms;
+        };
+        for (int G : {3, 4}) {
+            float ms = timeit([&] {
+                for (int t0 = 0; t0 + G <= P; t0 += G) {
+                    hipLaunchKernelGGL((k_check_msa<72, true, false>), dim3(M / 4, G), blk, 0, 0, d, scr, active, d_pos, M, E, (int64_t)t0, 1);
+                    hipLaunchKernelGGL((k_var_m<true, 8, true, false, 4>), dim3(N / 16, G), blk, 0, 0, scr, d, prior, hard, active, d_col_edge, (double*)nullptr, N, E, (int64_t)t0, rf, 1);
+                }
+            });
+            char nm[64];
+            std::snprintf(nm, sizeof nm, "msa fp64 c2v G=%d", G);
+            report(nm, ms, (double)iters * (P / G) * G);
+        }
+        uint8_t* codes = (uint8_t*)scr;
+        double* rec = (double*)(codes + (size_t)8 * E * 64);
+        for (int G : {2, 4}) {
+            for (int cpw : {2, 4}) {
+                const unsigned nb = (unsigned)(N / (4 * cpw)) * G;
+                float ms = timeit([&] {
+                    for (int t0 = 0; t0 + G <= P; t0 += G) {
+                        hipLaunchKernelGGL((k_check_msa_c<72, true>), dim3(M / 4, G), blk, 0, 0, d, codes, rec, active, M, E, (int64_t)t0, 1);
+                        if (cpw == 2) hipLaunchKernelGGL((k_var_msa_c<8, true, false, 2, true>), dim3(nb), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)t0, (uint32_t)G, rf, 1);
+                        else hipLaunchKernelGGL((k_var_msa_c<8, true, false, 4, true>), dim3(nb), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)t0, (uint32_t)G, rf, 1);
+                    }
+                });
+                char nm[64];
+                std::snprintf(nm, sizeof nm, "msa compressed SEL2 G=%d cpw=%d", G, cpw);
+                report(nm, ms, (double)iters * (P / G) * G);
+            }
+        }
+        for (int G : {1, 2, 4, 8}) {
+            for (int cpw : {2, 4}) {
+                const unsigned nb = (unsigned)(N / (4 * cpw)) * G;
+                float ms = timeit([&] {
+                    for (int t0 = 0; t0 + G <= P; t0 += G) {
+                        hipLaunchKernelGGL((k_check_msa_c<72, true>), dim3(M / 4, G), blk, 0, 0, d, codes, rec, active, M, E, (int64_t)t0, 1);
+                        if (cpw == 1) hipLaunchKernelGGL((k_var_msa_c<8, true, false, 1>), dim3(nb), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)t0, (uint32_t)G, rf, 1);
+                        else if (cpw == 2) hipLaunchKernelGGL((k_var_msa_c<8, true, false, 2>), dim3(nb), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)t0, (uint32_t)G, rf, 1);
+                        else hipLaunchKernelGGL((k_var_msa_c<8, true, false, 4>), dim3(nb), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)t0, (uint32_t)G, rf, 1);
+                    }
+                });
+                char nm[64];
+                std::snprintf(nm, sizeof nm, "msa compressed G=%d cpw=%d", G, cpw);
+                report(nm, ms, (double)iters * (P / G) * G);
+            }
+        }
+        // split for G=8 cpw=2
+        {
+            hipEvent_t a, b, c;
+            CK(hipEventCreate(&a));
+            CK(hipEventCreate(&b));
+            CK(hipEventCreate(&c));
+            float mc = 0, mv = 0;
+            for (int it = 0; it < 12; it++) {
+                CK(hipEventRecord(a));
+                hipLaunchKernelGGL((k_check_msa_c<72, true>), dim3(M / 4, 8), blk, 0, 0, d, codes, rec, active, M, E, (int64_t)0, 1);
+                CK(hipEventRecord(b));
+                hipLaunchKernelGGL((k_var_msa_c<8, true, false, 2>), dim3((unsigned)(N / 8) * 8), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)0, 8u, rf, 1);
+                CK(hipEventRecord(c));
+                CK(hipEventSynchronize(c));
+                float x, y;
+                CK(hipEventElapsedTime(&x, a, b));
+                CK(hipEventElapsedTime(&y, b, c));
+                if (it >= 2) { mc += x; mv += y; }
+            }
+            std::printf("msa compressed G=8 cpw=2 split: check %.2f us/tile, var %.2f us/tile\n", mc * 1e3 / 10 / 8, mv * 1e3 / 10 / 8);
+        }
+    }
+    // per-kernel split for the resident T=2 case
+    for (int T : {1, 2}) {
+        float mc = 0, mv = 0;
+        hipEvent_t a, b, c;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        CK(hipEventCreate(&c));
+        for (int it = 0; it < 20; it++) {
+            CK(hipEventRecord(a));
+            check(d, d, 0, T, false);
+            CK(hipEventRecord(b));
+            var(d, d, 0, T, false);
+            CK(hipEventRecord(c));
+            CK(hipEventSynchronize(c));
+            float x, y;
+            CK(hipEventElapsedTime(&x, a, b));
+            CK(hipEventElapsedTime(&y, b, c));
+            if (it >= 2) { mc += x; mv += y; }
+        }
+        std::printf("resident T=%d split: check %.2f us/tile, var %.2f us/tile\n", T, mc * 1e3 / 18 / T, mv * 1e3 / 18 / T);
+    }
+    return 0;
+}
