@@ -352,7 +352,7 @@ ldpc_engine* ldpc_engine_create_ex(const ldpc_graph* g, int32_t device, int32_t 
     if (!g) { set_error("null graph"); fail(LDPC_ERR_ARG, err); return nullptr; }
     auto e = std::make_unique<ldpc_engine>();
     e->e = std::make_unique<Engine>();
-    int rc = e->e->init(&g->h, device, algo, chunk, group_tiles, bit(0), bit(1), bit(2), bit(3));
+    int rc = e->e->init(&g->h, device, algo, chunk, group_tiles, bit(0), bit(1), bit(2), bit(3), bit(5));
     if (rc) { fail(rc, err); return nullptr; }
     if (err) *err = LDPC_OK;
     return e.release();
@@ -369,7 +369,7 @@ int ldpc_engine_info(ldpc_engine* e, int64_t* cap, int64_t* group_tiles, int32_t
     if (cap) *cap = e->e->cap;
     if (group_tiles) *group_tiles = e->e->group_tiles;
     if (flags) *flags = (e->e->nt_d ? 1 : 0) | (e->e->pipe ? 2 : 0) | (e->e->lr_csc ? 4 : 0) | (e->e->cont ? 8 : 0) |
-                        (e->e->msa_c ? 16 : 0);
+                        (e->e->msa_c ? 16 : 0) | (e->e->res ? 32 : 0);
     return LDPC_OK;
 }
 

@@ -42,6 +42,9 @@ constexpr int64_t kDefaultMsaGroupTiles = 4;  // LDPC_GROUP_TILES default for co
 constexpr int64_t kDefaultMsaPool = 1024;  // LDPC_MSA_POOL: resident lanes, compressed min-sum + continuous mode (A/B)
 constexpr int64_t kDefaultMsaC = 1;  // LDPC_MSA_C: compressed min-sum c2v (tools/icbench: 52.6 -> 33.5 us per tile-iteration)
 constexpr int64_t kDefaultVarCpw = 4;  // LDPC_VAR_CPW (A/B over two boxes: +2.6-2.9% over 1 column per wave)
+constexpr int64_t kDefaultRes = 0;       // LDPC_RES: resident in-place pool for BP / fp64 min-sum in continuous mode
+constexpr int64_t kDefaultResTiles = 2;  // LDPC_RES_TILES: pool tiles (tools/icbench: 2 x 85 MB fits the Infinity Cache)
+constexpr int64_t kDefaultResPoll = 4;   // LDPC_RES_POLL: steps between occupancy polls
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
@@ -72,7 +75,8 @@ Engine::~Engine()
     for (int i = 0; i < kRing; i++)
         if (ev_ring[i]) hipEventDestroy(ev_ring[i]);
     hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge); hipFree(d_col_row);
-    hipFree(v2c); hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
+    hipFree(d_unsat); hipFree(d_done);
+    hipFree(v2c); if (c2v != v2c) hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
     hipFree(post_t);
     if (stream) hipStreamDestroy(stream);
     if (stream2) hipStreamDestroy(stream2);
@@ -94,7 +98,7 @@ static int64_t env_int(const char* name, int64_t dflt)
 }
 
 int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, int64_t group, int nt, int pipelined,
-                 int csc, int cont_mode)
+                 int csc, int cont_mode, int res_mode)
 {
     g = graph;
     device = dev;
@@ -112,13 +116,26 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     msa_c = algo == LDPC_ALGO_MSA && reg_72_8 && nt != 0 && g->N % 16 == 0 && env_int("LDPC_MSA_C", kDefaultMsaC) != 0;
     if (cont_mode < 0) cont_mode = (int)env_int("LDPC_CONT", kDefaultCont);
     cont = cont_mode != 0 && !int_algo && reg_72_8;
+    // resident pool: a few tiles whose whole state fits the
+    // Infinity Cache, check->variable messages written over the variable->check
+    // messages they are computed from (each row's / column's edges are read
+    // into registers before its outputs are stored), no c2v scratch
+    if (res_mode < 0) res_mode = (int)env_int("LDPC_RES", kDefaultRes);
+    res = res_mode != 0 && cont && !msa_c;
+    if (res) {
+        nt = 0;  // the pool is meant to stay cached
+        pipelined = 0;
+        csc = 0;
+        res_poll = (int)std::max<int64_t>(1, env_int("LDPC_RES_POLL", kDefaultResPoll));
+    }
     if (chunk <= 0) {
         size_t fr = 0, tot = 0;
         LDPC_HIP(hipMemGetInfo(&fr, &tot));
         // half of the free memory for the resident state, at most 16384 codewords;
         // compressed min-sum in continuous mode: a small lane pool (its scattered
         // v2c stores run ~45 % longer over a 19 GB pool than over 1.2 GB, A/B)
-        const int64_t want = (msa_c && cont) ? env_int("LDPC_MSA_POOL", kDefaultMsaPool) : 16384;
+        const int64_t want = res ? 64 * env_int("LDPC_RES_TILES", kDefaultResTiles)
+                             : (msa_c && cont) ? env_int("LDPC_MSA_POOL", kDefaultMsaPool) : 16384;
         chunk = std::min<int64_t>(want, (int64_t)(fr / 2) / engine_bytes_per_codeword(*g));
     }
     cap = std::max<int64_t>(64, (chunk + 63) / 64 * 64);
@@ -127,7 +144,8 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     // group: tiles whose check->variable messages are live at once.  Small
     // groups keep c2v resident in the 256 MB Infinity Cache between the check
     // and the variable phase; 0 = the whole pass.
-    if (group < 0) group = env_int("LDPC_GROUP_TILES", msa_c ? kDefaultMsaGroupTiles : kDefaultGroupTiles);
+    if (res) group = 0;  // one launch per phase over the whole pool
+    else if (group < 0) group = env_int("LDPC_GROUP_TILES", msa_c ? kDefaultMsaGroupTiles : kDefaultGroupTiles);
     group_tiles = (group <= 0 || group > cap_tiles) ? cap_tiles : group;
     nt_d = nt != 0;
     if (pipelined < 0) pipelined = (int)env_int("LDPC_PIPE", kDefaultPipe);
@@ -178,8 +196,15 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     const size_t E = (size_t)std::max<int64_t>(g->E, 1);
     LDPC_HIP(hipMalloc((void**)&v2c, (size_t)cap * E * sizeof(double)));
     // continuous mode's drain tail (< 1/32 occupancy) launches wider groups
-    c2v_tiles = std::max<int64_t>((pipe ? 2 : 1) * group_tiles, cont ? (cap_tiles + 3) / 4 : 0);
-    LDPC_HIP(hipMalloc((void**)&c2v, (size_t)c2v_tiles * 64 * E * sizeof(double)));
+    if (res) {
+        c2v_tiles = cap_tiles;
+        c2v = v2c;  // in place
+        LDPC_HIP(hipMalloc((void**)&d_unsat, (size_t)cap_tiles * sizeof(unsigned long long)));
+        LDPC_HIP(hipMalloc((void**)&d_done, (size_t)cap_tiles * sizeof(unsigned int)));
+    } else {
+        c2v_tiles = std::max<int64_t>((pipe ? 2 : 1) * group_tiles, cont ? (cap_tiles + 3) / 4 : 0);
+        LDPC_HIP(hipMalloc((void**)&c2v, (size_t)c2v_tiles * 64 * E * sizeof(double)));
+    }
     LDPC_HIP(hipMalloc((void**)&prior, (size_t)cap * g->N * sizeof(double)));
     LDPC_HIP(hipMalloc((void**)&hard, (size_t)cap_tiles * g->N * sizeof(uint64_t)));
     LDPC_HIP(hipMalloc((void**)&active, (size_t)cap_tiles * sizeof(uint64_t)));
@@ -328,36 +353,41 @@ static void var_regular3(int algo, hipStream_t s, dim3 grid, const double* scrat
                            col_edge, pt, N, E, t0, rf);
 }
 
-template <bool MSA, int CPW>
+template <bool MSA, bool NT, int CPW>
 static void var_multi2(hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior, uint64_t* hard,
                        const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E, int64_t t0,
                        const dev::Refill& rf, int full)
 {
     using namespace dev;
     if (rf.fresh)
-        hipLaunchKernelGGL((k_var_m<MSA, 8, true, true, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
+        hipLaunchKernelGGL((k_var_m<MSA, 8, NT, true, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
                            col_edge, pt, N, E, t0, rf, full);
     else
-        hipLaunchKernelGGL((k_var_m<MSA, 8, true, false, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
+        hipLaunchKernelGGL((k_var_m<MSA, 8, NT, false, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
                            col_edge, pt, N, E, t0, rf, full);
 }
 
-template <bool MSA>
+template <bool MSA, bool NT>
 static void var_multi1(int cpw, hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior,
                        uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E,
                        int64_t t0, const dev::Refill& rf, int full)
 {
-    if (cpw == 2) var_multi2<MSA, 2>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
-    else if (cpw == 4) var_multi2<MSA, 4>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
-    else var_multi2<MSA, 8>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    if (cpw == 2) var_multi2<MSA, NT, 2>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    else if (cpw == 4) var_multi2<MSA, NT, 4>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    else var_multi2<MSA, NT, 8>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
 }
 
-static void var_multi(int algo, int cpw, hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior,
-                      uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E,
-                      int64_t t0, const dev::Refill& rf, int full)
+static void var_multi(int algo, bool nt, int cpw, hipStream_t s, dim3 grid, const double* scratch, double* v2c,
+                      double* prior, uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt,
+                      int32_t N, int64_t E, int64_t t0, const dev::Refill& rf, int full)
 {
-    if (algo == LDPC_ALGO_MSA) var_multi1<true>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
-    else var_multi1<false>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    if (algo == LDPC_ALGO_MSA) {
+        if (nt) var_multi1<true, true>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+        else var_multi1<true, false>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    } else {
+        if (nt) var_multi1<false, true>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+        else var_multi1<false, false>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    }
 }
 
 template <bool NT, bool CSCL>
@@ -440,9 +470,9 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         });
         return LDPC_OK;
     }
-    if (reg8 && var_cpw > 1 && nt_d && !lr_csc && N % (4 * var_cpw) == 0) {
+    if (reg8 && var_cpw > 1 && (nt_d || res) && !lr_csc && N % (4 * var_cpw) == 0) {
         const dim3 gm((unsigned)(N / (4 * var_cpw)), gt);
-        LAUNCH_ON(s, K_VAR, var_multi(algo, var_cpw, s, gm, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf, full_lanes));
+        LAUNCH_ON(s, K_VAR, var_multi(algo, nt_d, var_cpw, s, gm, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf, full_lanes));
         return LDPC_OK;
     }
     if (reg8) {
@@ -662,6 +692,42 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     ContOut co{d_hard, d_post, d_iters, d_valid, post_t, prior, msa, post_kind == LDPC_POST_RATIO ? 1 : 0};
     const Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0};
     const bool reg_rowT = d_col_idx_T != nullptr;
+    if (res) {
+        // resident pool: every step is syndrome + check + variable over the
+        // whole pool, messages in place; the occupancy is read every
+        // res_poll steps (kLag polls behind the device)
+        LDPC_HIP(hipMemsetAsync(d_unsat, 0, (size_t)tiles * sizeof(unsigned long long), stream));
+        LDPC_HIP(hipMemsetAsync(d_done, 0, (size_t)tiles * sizeof(unsigned int), stream));
+        const unsigned syn_blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (2 * (int64_t)M + 255) / 256));
+        const dim3 g_syn(syn_blocks, (unsigned)tiles);
+        for (int64_t s = 0;; s++) {
+            const bool poll = (s % res_poll) == res_poll - 1;
+            const int64_t pi = s / res_poll;
+            const int slot = (int)(pi % kRing);
+            cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
+            if (poll) LDPC_HIP(hipMemsetAsync(cs.occ_count, 0, sizeof(unsigned long long), stream));
+            if (reg_rowT)
+                LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome_res<72>, g_syn, dim3(256), 0, stream, hard, d_row_ptr,
+                                                 d_col_idx, d_col_idx_T, M, N, max_iter, cs, co, d_unsat, d_done));
+            else
+                LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome_res<0>, g_syn, dim3(256), 0, stream, hard, d_row_ptr,
+                                                 d_col_idx, d_col_idx_T, M, N, max_iter, cs, co, d_unsat, d_done));
+            if (poll) {
+                LDPC_HIP(hipMemcpyAsync(h_occ + slot, cs.occ_count, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                        stream));
+                LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
+            }
+            int rc;
+            if ((rc = launch_check(stream, v2c, 0, (unsigned)tiles))) return rc;
+            if ((rc = launch_var(stream, v2c, 0, (unsigned)tiles, pt, rf))) return rc;
+            if (poll && pi >= kLag) {
+                const int old = (int)((pi - kLag) % kRing);
+                LDPC_HIP(hipEventSynchronize(ev_ring[old]));
+                if (h_occ[old] == 0) break;
+            }
+        }
+        return LDPC_OK;
+    }
     // While the pool is mostly occupied, launch per tile group (c2v stays in the
     // Infinity Cache); once the input is drained and few lanes remain, one
     // check + one variable launch over all tiles per step (the tail is launch-

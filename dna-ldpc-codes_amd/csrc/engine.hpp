@@ -45,6 +45,10 @@ struct Engine {
     int full_lanes = 0;       // all lanes of an active tile store (whole cache lines)
     int var_cpw = 1;          // variable phase: columns per wave (k_var_m when > 1)
     bool msa_c = false;       // min-sum with compressed c2v (records + codes, k_check_msa_c / k_var_msa_c)
+    bool res = false;         // resident pool: a few tiles iterated in place (c2v overwrites v2c), k_syndrome_res
+    int res_poll = 4;         // res: steps between occupancy polls
+    unsigned long long* d_unsat = nullptr;  // res: [tile] syndrome words of the step
+    unsigned int* d_done = nullptr;         // res: [tile] syndrome blocks arrived
     static constexpr int kRing = 8, kLag = 2;
     uint64_t* d_fresh = nullptr;
     uint64_t* d_occ = nullptr;
@@ -87,7 +91,7 @@ struct Engine {
 
     ~Engine();
     int init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, int64_t group = -1, int nt = -1,
-             int pipelined = -1, int csc = -1, int cont_mode = -1);
+             int pipelined = -1, int csc = -1, int cont_mode = -1, int res_mode = -1);
     int run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
                  int post_kind, int32_t* d_iters, uint8_t* d_valid);
     // decode Bc <= cap codewords whose [Bc][N] input is at d_in (device)

@@ -979,6 +979,73 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ pos
 // Which lane decodes which codeword varies run to run; each codeword's
 // arithmetic does not.
 // ---------------------------------------------------------------------------
+// Lane bookkeeping of tile t once its syndrome word U is known (threads 0..63
+// of the block; lane = threadIdx.x).  Shared with k_syndrome_res.
+__device__ __forceinline__ void cont_lanes(int64_t t, uint64_t occ, uint64_t U, int32_t max_iter, const ContState& cs,
+                                           const ContOut& co, int64_t* s_b, int32_t* s_n, uint64_t* s_fin)
+{
+    const int lane = lane_id();
+    {
+        const size_t li = (size_t)t * TILE + lane;
+        const bool o = (occ >> lane) & 1ull;
+        const int32_t ln = o ? cs.lane_n[li] : 0;
+        const bool unsat = (U >> lane) & 1ull;
+        const bool fin = o && (!unsat || ln == max_iter);
+        const bool cont = o && !fin;
+        const int64_t b = o ? cs.lane_b[li] : -1;
+        if (fin) { co.iters[b] = ln; co.valid[b] = unsat ? 0 : 1; }
+        s_b[lane] = b;
+        s_n[lane] = ln;
+        const uint64_t F = __ballot(fin), Cm = __ballot(cont);
+        // refill every lane that is not continuing
+        const uint64_t freem = ~Cm;
+        const int nfree = __popcll(freem);
+        unsigned long long base = 0;
+        if (lane == 0) {
+            const unsigned long long nb = __hip_atomic_load(cs.next_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            base = (nb < (unsigned long long)cs.B) ? atomicAdd(cs.next_b, (unsigned long long)nfree) : nb;
+        }
+        base = __shfl(base, 0);
+        const int rank = __popcll(freem & ((1ull << lane) - 1ull));
+        const bool fresh = !cont && (base + (unsigned long long)rank < (unsigned long long)cs.B);
+        const uint64_t Fr = __ballot(fresh);
+        if (cont) cs.lane_n[li] = ln + 1;
+        if (fresh) { cs.lane_b[li] = (int64_t)(base + rank); cs.lane_n[li] = 0; }
+        if (lane == 0) {
+            cs.active[t] = Cm;
+            cs.fresh[t] = Fr;
+            cs.occupied[t] = Cm | Fr;
+            *s_fin = F;
+            if ((Cm | Fr) && cs.occ_count) atomicAdd(cs.occ_count, (unsigned long long)__popcll(Cm | Fr));
+        }
+    }
+}
+
+// The finished codewords' outputs (hard bits of this step, posterior), all
+// threads of the block.
+__device__ __forceinline__ void cont_outputs(int64_t t, uint64_t F, const uint64_t* __restrict__ h, int32_t N,
+                                             const ContOut& co, const int64_t* s_b, const int32_t* s_n)
+{
+    for (int32_t j = threadIdx.x; j < N; j += blockDim.x) {
+        const uint64_t wj = h[j];
+        for (uint64_t f = F; f; f &= f - 1) {
+            const int l = __builtin_ctzll(f);
+            const size_t ob = (size_t)s_b[l] * N + j;
+            co.hard[ob] = (uint8_t)((wj >> l) & 1ull);
+            if (co.post) {
+                const size_t pj = ((size_t)t * N + j) * TILE + l;
+                const double pv = s_n[l] > 0 ? co.post_t[pj] : co.prior[pj];
+                if (co.algo_msa) co.post[ob] = pv;
+                else {
+                    const double P = __builtin_isnan(pv) ? 1.0 : pv;
+                    co.post[ob] = co.post_ratio ? P : log(P);
+                }
+            }
+        }
+    }
+}
+
+// one block per tile
 template <int DC>
 __global__ __launch_bounds__(1024) void k_syndrome_cont(const uint64_t* __restrict__ hard,
                                                         const int32_t* __restrict__ row_ptr,
@@ -1015,60 +1082,83 @@ __global__ __launch_bounds__(1024) void k_syndrome_cont(const uint64_t* __restri
         uint64_t U = 0;
         if (occ)
             for (int q = 0; q < (int)(blockDim.x >> 6); ++q) U |= red[q];
-        const size_t li = (size_t)t * TILE + lane;
-        const bool o = (occ >> lane) & 1ull;
-        const int32_t ln = o ? cs.lane_n[li] : 0;
-        const bool unsat = (U >> lane) & 1ull;
-        const bool fin = o && (!unsat || ln == max_iter);
-        const bool cont = o && !fin;
-        const int64_t b = o ? cs.lane_b[li] : -1;
-        if (fin) { co.iters[b] = ln; co.valid[b] = unsat ? 0 : 1; }
-        s_b[lane] = b;
-        s_n[lane] = ln;
-        const uint64_t F = __ballot(fin), Cm = __ballot(cont);
-        // refill every lane that is not continuing
-        const uint64_t freem = ~Cm;
-        const int nfree = __popcll(freem);
-        unsigned long long base = 0;
-        if (lane == 0) {
-            const unsigned long long nb = __hip_atomic_load(cs.next_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            base = (nb < (unsigned long long)cs.B) ? atomicAdd(cs.next_b, (unsigned long long)nfree) : nb;
+        cont_lanes(t, occ, U, max_iter, cs, co, s_b, s_n, &s_fin);
+    }
+    __syncthreads();
+    if (s_fin) cont_outputs(t, s_fin, h, N, co, s_b, s_n);
+}
+
+// ---------------------------------------------------------------------------
+// Resident-pool syndrome step (engine `res` mode: a pool of a few tiles,
+// iterated in place).  One block per tile would leave a 2-tile pool's
+// syndrome a long serial chain, so a tile's rows are spread over gridDim.x
+// blocks (two threads per row, DC/2 gathers each); every block ORs its
+// parities into unsat[t], and the last block of the tile to arrive (counter
+// done[t]) runs the lane bookkeeping and output writes of k_syndrome_cont,
+// then re-arms unsat[t] / done[t] for the next step.  grid (blocks, tiles),
+// block 256.
+// ---------------------------------------------------------------------------
+template <int DC>
+__global__ __launch_bounds__(256) void k_syndrome_res(const uint64_t* __restrict__ hard,
+                                                      const int32_t* __restrict__ row_ptr,
+                                                      const int32_t* __restrict__ col_idx,
+                                                      const int32_t* __restrict__ col_idx_T, int32_t M, int32_t N,
+                                                      int32_t max_iter, ContState cs, ContOut co,
+                                                      unsigned long long* __restrict__ unsat,
+                                                      unsigned int* __restrict__ done)
+{
+    __shared__ uint64_t red[4];
+    __shared__ int64_t s_b[TILE];
+    __shared__ int32_t s_n[TILE];
+    __shared__ uint64_t s_fin;
+    __shared__ int s_last;
+    const int64_t t = blockIdx.y;
+    const uint64_t occ = cs.occupied[t];
+    const int lane = lane_id(), w = wave_id();
+    const uint64_t* h = hard + (size_t)t * N;
+    uint64_t u = 0;
+    if (occ) {
+        const int half = threadIdx.x & 1;
+        for (int32_t i = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 1); i < M;
+             i += (int32_t)((gridDim.x * blockDim.x) >> 1)) {
+            uint64_t p = 0;
+            if (DC > 0) {
+                constexpr int H = (DC + 1) / 2;
+                const int k0 = half * H;
+#pragma unroll
+                for (int k = 0; k < H; ++k)
+                    if (k0 + k < DC) p ^= h[col_idx_T[(size_t)(k0 + k) * M + i]];
+            } else {
+                for (int32_t e = row_ptr[i] + half; e < row_ptr[i + 1]; e += 2) p ^= h[col_idx[e]];
+            }
+            p ^= shfl_xor_u64(p, 1);  // the row's parity: XOR of both halves
+            u |= p;
         }
-        base = __shfl(base, 0);
-        const int rank = __popcll(freem & ((1ull << lane) - 1ull));
-        const bool fresh = !cont && (base + (unsigned long long)rank < (unsigned long long)cs.B);
-        const uint64_t Fr = __ballot(fresh);
-        if (cont) cs.lane_n[li] = ln + 1;
-        if (fresh) { cs.lane_b[li] = (int64_t)(base + rank); cs.lane_n[li] = 0; }
-        if (lane == 0) {
-            cs.active[t] = Cm;
-            cs.fresh[t] = Fr;
-            cs.occupied[t] = Cm | Fr;
-            s_fin = F;
-            if (Cm | Fr) atomicAdd(cs.occ_count, (unsigned long long)__popcll(Cm | Fr));
+#pragma unroll
+        for (int off = 32; off > 1; off >>= 1) u |= shfl_xor_u64(u, off);
+    }
+    if (lane == 0) red[w] = u;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t U = 0;
+        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) U |= red[q];
+        if (U) atomicOr(unsat + t, (unsigned long long)U);
+        __threadfence();
+        s_last = atomicAdd(done + t, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    if (threadIdx.x < 64) {
+        const uint64_t U = __hip_atomic_load(unsat + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cont_lanes(t, occ, occ ? U : 0ull, max_iter, cs, co, s_b, s_n, &s_fin);
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(unsat + t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
-    // write the finished codewords' outputs (hard bits of this step, posterior)
-    uint64_t F = s_fin;
-    if (!F) return;
-    for (int32_t j = threadIdx.x; j < N; j += blockDim.x) {
-        const uint64_t wj = h[j];
-        for (uint64_t f = F; f; f &= f - 1) {
-            const int l = __builtin_ctzll(f);
-            const size_t ob = (size_t)s_b[l] * N + j;
-            co.hard[ob] = (uint8_t)((wj >> l) & 1ull);
-            if (co.post) {
-                const size_t pj = ((size_t)t * N + j) * TILE + l;
-                const double pv = s_n[l] > 0 ? co.post_t[pj] : co.prior[pj];
-                if (co.algo_msa) co.post[ob] = pv;
-                else {
-                    const double P = __builtin_isnan(pv) ? 1.0 : pv;
-                    co.post[ob] = co.post_ratio ? P : log(P);
-                }
-            }
-        }
-    }
+    if (s_fin) cont_outputs(t, s_fin, h, N, co, s_b, s_n);
 }
 
 // hard ballots -> [b][N] u8 (the reference's dblk / dec_*.txt bits)

@@ -409,11 +409,12 @@ class DeviceBuffer:
 class Engine:
     def __init__(self, g: Graph, device: int = 0, algo="bp", chunk: int = 0, group_tiles: int = -1,
                  nontemporal: Optional[bool] = None, pipeline: Optional[bool] = None,
-                 csc_scratch: Optional[bool] = None, continuous: Optional[bool] = None):
+                 csc_scratch: Optional[bool] = None, continuous: Optional[bool] = None,
+                 resident: Optional[bool] = None):
         self.g, self.device, self.algo = g, device, _algo(algo)
         err = C.c_int(0)
         flags_set = flags = 0
-        for bit, v in enumerate((nontemporal, pipeline, csc_scratch, continuous)):
+        for bit, v in zip((0, 1, 2, 3, 5), (nontemporal, pipeline, csc_scratch, continuous, resident)):
             if v is not None:
                 flags_set |= 1 << bit
                 flags |= int(bool(v)) << bit
@@ -427,6 +428,7 @@ class Engine:
         self.nontemporal, self.pipeline, self.csc_scratch = bool(fl.value & 1), bool(fl.value & 2), bool(fl.value & 4)
         self.continuous = bool(fl.value & 8)
         self.msa_compressed = bool(fl.value & 16)  # min-sum c2v as per-row records + per-edge codes
+        self.resident = bool(fl.value & 32)  # in-place pool of a few tiles (LDPC_RES)
 
     def decode(self, d_in, in_kind: int, B: int, max_iter: int, d_hard=None, d_post=None, post_kind=POST_LLR,
                d_iters=None, d_valid=None):

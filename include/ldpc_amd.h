@@ -167,7 +167,9 @@ ldpc_engine *ldpc_engine_create(const ldpc_graph *g, int32_t device, int32_t alg
  * check(g+1) with variable(g) on a second stream, bit 2 = check->variable
  * messages stored in column order, bit 3 = continuous batching (a finished
  * codeword's lane is refilled with the next one; needs hard/iters/valid
- * outputs) (env LDPC_NT_D, LDPC_PIPE, LDPC_LR_CSC, LDPC_CONT). */
+ * outputs), bit 5 = resident pool (continuous BP / fp64 min-sum: a pool of
+ * LDPC_RES_TILES tiles iterated in place, sized for the Infinity Cache)
+ * (env LDPC_NT_D, LDPC_PIPE, LDPC_LR_CSC, LDPC_CONT, LDPC_RES). */
 ldpc_engine *ldpc_engine_create_ex(const ldpc_graph *g, int32_t device, int32_t algo, int64_t chunk,
                                    int64_t group_tiles, int32_t flags_set, int32_t flags, int *err);
 void ldpc_engine_free(ldpc_engine *e);
@@ -211,7 +213,7 @@ int ldpc_engine_set_params(ldpc_engine *e, int32_t msa_precision, double msa_ste
 /* The schedule an engine runs with: resident codewords per pass (the lane
  * pool in continuous mode), group tiles, and flags with the bits of
  * ldpc_engine_create_ex plus bit 4 = compressed min-sum check->variable
- * messages (env LDPC_MSA_C). */
+ * messages (env LDPC_MSA_C); bit 5 as in create_ex. */
 int ldpc_engine_info(ldpc_engine *e, int64_t *cap, int64_t *group_tiles, int32_t *flags);
 int ldpc_engine_stats(ldpc_engine *e, ldpc_kernel_stats *out);
 

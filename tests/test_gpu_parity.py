@@ -288,6 +288,44 @@ def test_variable_columns_per_wave_bitexact(gpu, og, codewords, monkeypatch, cpw
     _cmp(G2, og, llr, 30, algo="msa")
 
 
+@pytest.mark.parametrize("res,tiles,poll,cpw", [(1, 2, 4, 4), (1, 1, 1, 4), (1, 3, 2, 2), (1, 2, 7, 1), (0, 2, 4, 4)])
+def test_resident_pool_in_place_bitexact(gpu, og, codewords, monkeypatch, res, tiles, poll, cpw):
+    """Resident pool (engine.hip run_cont `res`, kernels.hpp k_syndrome_res):
+    a pool of 1-3 tiles iterated in place (check->variable messages written
+    over the variable->check messages of the same edges), the syndrome spread
+    over several blocks per tile with last-block lane bookkeeping, occupancy
+    polled every `poll` steps.  BP and fp64 min-sum stay bit-exact across
+    mixed early exits, all lanes finishing at once (p = 0.02, exactly 50
+    iterations), max_iter 0, batches smaller than the pool, NaN / inf inputs."""
+    monkeypatch.setenv("LDPC_RES", str(res))
+    monkeypatch.setenv("LDPC_RES_TILES", str(tiles))
+    monkeypatch.setenv("LDPC_RES_POLL", str(poll))
+    monkeypatch.setenv("LDPC_VAR_CPW", str(cpw))
+    monkeypatch.setenv("LDPC_MSA_C", "0")
+    monkeypatch.setenv("LDPC_CONT", "1")
+    G2 = gpu.Graph(PCHK)
+    llr = synth.dna_like_llrs(codewords, seed=1, reads=57000)[:200]
+    _cmp(G2, og, llr, 60)
+    llr = np.concatenate([synth.bsc_llrs(codewords, 0, 150, seed=3, p=0.003),
+                          synth.bsc_llrs(codewords, 150, 130, seed=2026, p=0.02)])
+    _, _, it, _ = _cmp(G2, og, llr, 50)
+    assert (it[150:] == 50).all() and len(np.unique(it[:150])) > 2
+    _cmp(G2, og, llr[:70], 0)
+    _cmp(G2, og, llr[:5], 50)
+    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 200, seed=8, p=0.002), 30, algo="msa")
+    rng = np.random.default_rng(21)
+    llr = synth.dna_like_llrs(codewords, seed=2, reads=60000)[:100]
+    llr[rng.random(llr.shape) < 0.002] = np.nan
+    llr[rng.random(llr.shape) < 0.002] = np.inf
+    llr[rng.random(llr.shape) < 0.002] = -np.inf
+    ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 40, algo=0, post_mode=1, threads=8)
+    h, p, it, v = G2.decode(llr, max_iter=40, algo="bp", post="ratio")
+    assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
+    nan = np.isnan(ref_p)
+    assert np.array_equal(np.isnan(p), nan)
+    assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64))
+
+
 @pytest.mark.parametrize("chunk", [64, 128])
 def test_continuous_batching_edge_cases(gpu, og, codewords, monkeypatch, chunk):
     """Continuous mode with a pool smaller than the batch (lanes are refilled
