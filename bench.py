@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--nt", type=int, default=-1, help="nontemporal d-stream (-1: engine default)")
     ap.add_argument("--pipe", type=int, default=-1, help="two-stream check/variable overlap (-1: engine default)")
     ap.add_argument("--cont", type=int, default=-1, help="continuous batching / lane refill (-1: engine default)")
+    ap.add_argument("--res", type=int, default=-1,
+                    help="resident in-place pool of a few tiles (-1: engine default; BP / fp64 min-sum, continuous)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
     ap.add_argument("--workload", default="bsc", choices=["bsc", "dna272"],
                     help="bsc: SURVEY 8(d) configs 3-5 (default); dna272: config 2, the 272-codeword DNA batch")
@@ -176,7 +178,8 @@ def main():
     algo = args.algo
     eng = L.Engine(G, dev, algo, chunk=args.chunk, group_tiles=args.group_tiles,
                    nontemporal=None if args.nt < 0 else bool(args.nt), pipeline=None if args.pipe < 0 else bool(args.pipe),
-                   continuous=None if args.cont < 0 else bool(args.cont))
+                   continuous=None if args.cont < 0 else bool(args.cont),
+                   resident=None if args.res < 0 else bool(args.res))
     cw = synth.load_codewords()
     d_cw = L.DeviceBuffer(dev, cw.nbytes)
     d_cw.upload(cw)
@@ -273,7 +276,8 @@ def main():
                    "batch_per_gpu": B, "global_batch": int(total_cw / args.steps), "max_iter": args.max_iter,
                    "algo": algo, "parallelism": f"dp{world} (contiguous codeword shards, no collective)",
                    "resident_per_pass": eng.cap, "group_tiles": eng.group_tiles, "nontemporal_d": eng.nontemporal,
-                   "two_stream": eng.pipeline, "continuous": eng.continuous,
+                   "two_stream": eng.pipeline, "continuous": eng.continuous, "resident_pool": eng.resident,
+                   "compressed_msa": eng.msa_compressed,
                    "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 4)},
         "roofline": roof,
     }

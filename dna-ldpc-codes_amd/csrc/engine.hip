@@ -42,9 +42,9 @@ constexpr int64_t kDefaultMsaGroupTiles = 4;  // LDPC_GROUP_TILES default for co
 constexpr int64_t kDefaultMsaPool = 1024;  // LDPC_MSA_POOL: resident lanes, compressed min-sum + continuous mode (A/B)
 constexpr int64_t kDefaultMsaC = 1;  // LDPC_MSA_C: compressed min-sum c2v (tools/icbench: 52.6 -> 33.5 us per tile-iteration)
 constexpr int64_t kDefaultVarCpw = 4;  // LDPC_VAR_CPW (A/B over two boxes: +2.6-2.9% over 1 column per wave)
-constexpr int64_t kDefaultRes = 0;       // LDPC_RES: resident in-place pool for BP / fp64 min-sum in continuous mode
-constexpr int64_t kDefaultResTiles = 2;  // LDPC_RES_TILES: pool tiles (tools/icbench: 2 x 85 MB fits the Infinity Cache)
-constexpr int64_t kDefaultResPoll = 4;   // LDPC_RES_POLL: steps between occupancy polls
+constexpr int64_t kDefaultRes = 1;       // LDPC_RES: resident in-place pool for BP / fp64 min-sum in continuous mode
+constexpr int64_t kDefaultResTiles = 3;  // LDPC_RES_TILES: pool tiles (3 x 85 MB ~ the 256 MB Infinity Cache; A/B)
+constexpr int64_t kDefaultResPoll = 8;   // LDPC_RES_POLL: steps between occupancy polls
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
@@ -75,7 +75,7 @@ Engine::~Engine()
     for (int i = 0; i < kRing; i++)
         if (ev_ring[i]) hipEventDestroy(ev_ring[i]);
     hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge); hipFree(d_col_row);
-    hipFree(d_unsat); hipFree(d_done);
+    hipFree(d_unsat); hipFree(d_done); hipFree(d_fin); hipFree(d_fin_b); hipFree(d_fin_n);
     hipFree(v2c); if (c2v != v2c) hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
     hipFree(post_t);
     if (stream) hipStreamDestroy(stream);
@@ -121,7 +121,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     // messages they are computed from (each row's / column's edges are read
     // into registers before its outputs are stored), no c2v scratch
     if (res_mode < 0) res_mode = (int)env_int("LDPC_RES", kDefaultRes);
-    res = res_mode != 0 && cont && !msa_c;
+    res = res_mode != 0 && cont && !msa_c && g->N % 32 == 0;  // k_var_m at any columns-per-wave
     if (res) {
         nt = 0;  // the pool is meant to stay cached
         pipelined = 0;
@@ -201,6 +201,9 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         c2v = v2c;  // in place
         LDPC_HIP(hipMalloc((void**)&d_unsat, (size_t)cap_tiles * sizeof(unsigned long long)));
         LDPC_HIP(hipMalloc((void**)&d_done, (size_t)cap_tiles * sizeof(unsigned int)));
+        LDPC_HIP(hipMalloc((void**)&d_fin, (size_t)cap_tiles * sizeof(uint64_t)));
+        LDPC_HIP(hipMalloc((void**)&d_fin_b, (size_t)cap * sizeof(int64_t)));
+        LDPC_HIP(hipMalloc((void**)&d_fin_n, (size_t)cap * sizeof(int32_t)));
     } else {
         c2v_tiles = std::max<int64_t>((pipe ? 2 : 1) * group_tiles, cont ? (cap_tiles + 3) / 4 : 0);
         LDPC_HIP(hipMalloc((void**)&c2v, (size_t)c2v_tiles * 64 * E * sizeof(double)));
@@ -211,8 +214,59 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     LDPC_HIP(hipMalloc((void**)&iters, (size_t)cap * sizeof(int32_t)));
     LDPC_HIP(hipMalloc((void**)&valid, (size_t)cap * sizeof(uint8_t)));
     const int probes = (int)env_int("LDPC_C2V_PROBE", kDefaultC2vProbe);
+    if (probes > 1 && res) return probe_res(probes);
     if (probes > 1 && !int_algo && group_tiles < cap_tiles) return probe_c2v(probes);
     return LDPC_OK;
+}
+
+// Resident pool: the same placement probe for the in-place message pool
+// (v2c, ~226 MB at 3 tiles, sized to the 256 MB Infinity Cache): time one
+// in-place check + variable step of the whole pool on each candidate
+// allocation (state zeroed, results discarded), keep the fastest.
+int Engine::probe_res(int probes)
+{
+    const size_t E = (size_t)std::max<int64_t>(g->E, 1);
+    const size_t bytes = (size_t)cap * E * sizeof(double);
+    const unsigned gt = (unsigned)cap_tiles;
+    LDPC_HIP(hipMemsetAsync(prior, 0, (size_t)cap * g->N * sizeof(double), stream));
+    LDPC_HIP(hipMemsetAsync(active, 0xff, (size_t)cap_tiles * sizeof(uint64_t), stream));
+    std::vector<double*> cand{v2c};
+    for (int i = 1; i < probes; i++) {
+        double* p = nullptr;
+        if (hipMalloc((void**)&p, bytes) != hipSuccess) { (void)hipGetLastError(); break; }
+        cand.push_back(p);
+    }
+    for (double* p : cand) LDPC_HIP(hipMemsetAsync(p, 0, bytes, stream));
+    hipEvent_t e0, e1;
+    LDPC_HIP(hipEventCreate(&e0));
+    LDPC_HIP(hipEventCreate(&e1));
+    const int saved_stride = profile_stride;
+    profile_stride = 0;
+    size_t best = 0;
+    float best_ms = 1e30f;
+    int rc = LDPC_OK;
+    for (size_t c = 0; c < cand.size() && rc == LDPC_OK; c++) {
+        v2c = c2v = cand[c];
+        for (int rep = 0; rep < 5 && rc == LDPC_OK; rep++) {  // rep 0 warms up
+            if (rep == 1 && hipEventRecord(e0, stream) != hipSuccess) rc = LDPC_ERR_DEVICE;
+            if (!rc) rc = launch_check(stream, v2c, 0, gt);  // rstep == nullptr: plain in-place check
+            if (!rc) rc = launch_var(stream, v2c, 0, gt, nullptr, dev::Refill{});
+        }
+        if (rc) break;
+        LDPC_HIP(hipEventRecord(e1, stream));
+        LDPC_HIP(hipEventSynchronize(e1));
+        float ms = 0;
+        LDPC_HIP(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best_ms) { best_ms = ms; best = c; }
+    }
+    profile_stride = saved_stride;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    for (size_t c = 0; c < cand.size(); c++)
+        if (c != best) (void)hipFree(cand[c]);
+    v2c = c2v = cand[best];
+    for (int k = 0; k < K_NCLASS; k++) launches[k] = 0;
+    return rc;
 }
 
 // The check->variable scratch of one tile group (~226 MB at G = 3) is meant
@@ -334,9 +388,11 @@ static void check_regular(int algo, hipStream_t s, dim3 grid, const double* v2c,
 {
     using namespace dev;
     if (algo == LDPC_ALGO_BP)
-        hipLaunchKernelGGL((k_check_bp<72, NT, CSCL>), grid, dim3(256), 0, s, v2c, scratch, active, pos, M, E, t0, full);
+        hipLaunchKernelGGL((k_check_bp<72, NT, CSCL, false>), grid, dim3(256), 0, s, v2c, scratch, active, pos, M, E,
+                           t0, full, ResStep{});
     else
-        hipLaunchKernelGGL((k_check_msa<72, NT, CSCL>), grid, dim3(256), 0, s, v2c, scratch, active, pos, M, E, t0, full);
+        hipLaunchKernelGGL((k_check_msa<72, NT, CSCL, false>), grid, dim3(256), 0, s, v2c, scratch, active, pos, M, E,
+                           t0, full, ResStep{});
 }
 
 template <bool NT, bool CSCL, bool CONT>
@@ -372,7 +428,8 @@ static void var_multi1(int cpw, hipStream_t s, dim3 grid, const double* scratch,
                        uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E,
                        int64_t t0, const dev::Refill& rf, int full)
 {
-    if (cpw == 2) var_multi2<MSA, NT, 2>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    if (cpw == 1) var_multi2<MSA, NT, 1>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    else if (cpw == 2) var_multi2<MSA, NT, 2>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
     else if (cpw == 4) var_multi2<MSA, NT, 4>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
     else var_multi2<MSA, NT, 8>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
 }
@@ -430,6 +487,15 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
     const int64_t E = g->E;
     const bool reg72 = g->regular_dc && g->dc_max == 72;
     const dim3 grid((M + 3) / 4, gt), blk(256);
+    if (res && rstep) {  // resident pool: syndrome + lane bookkeeping fused (ResStep)
+        if (algo == LDPC_ALGO_BP)
+            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_bp<72, false, false, true>), grid, blk, 0, s, v2c, scratch,
+                                                     active, d_csc_pos, M, E, t0, full_lanes, *rstep));
+        else
+            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa<72, false, false, true>), grid, blk, 0, s, v2c,
+                                                     scratch, active, d_csc_pos, M, E, t0, full_lanes, *rstep));
+        return LDPC_OK;
+    }
     if (msa_c) {
         LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa_c<72, true>), grid, blk, 0, s, v2c, msa_codes(scratch),
                                                  msa_rec(scratch, c2v_tiles, E), active, M, E, t0, full_lanes));
@@ -470,7 +536,8 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         });
         return LDPC_OK;
     }
-    if (reg8 && var_cpw > 1 && (nt_d || res) && !lr_csc && N % (4 * var_cpw) == 0) {
+    // (the resident pool always takes k_var_m: it writes the finished lanes' outputs)
+    if (reg8 && (res || (var_cpw > 1 && nt_d)) && !lr_csc && N % (4 * var_cpw) == 0) {
         const dim3 gm((unsigned)(N / (4 * var_cpw)), gt);
         LAUNCH_ON(s, K_VAR, var_multi(algo, nt_d, var_cpw, s, gm, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf, full_lanes));
         return LDPC_OK;
@@ -693,40 +760,39 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     const Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0};
     const bool reg_rowT = d_col_idx_T != nullptr;
     if (res) {
-        // resident pool: every step is syndrome + check + variable over the
-        // whole pool, messages in place; the occupancy is read every
-        // res_poll steps (kLag polls behind the device)
+        // resident pool: every step is check (+ the syndrome of the previous
+        // step and the lane bookkeeping, ResStep) then variable (+ the
+        // finished codewords' outputs) over the whole pool, messages in place;
+        // the occupancy is read every res_poll steps, kLag polls behind
         LDPC_HIP(hipMemsetAsync(d_unsat, 0, (size_t)tiles * sizeof(unsigned long long), stream));
         LDPC_HIP(hipMemsetAsync(d_done, 0, (size_t)tiles * sizeof(unsigned int), stream));
-        const unsigned syn_blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (2 * (int64_t)M + 255) / 256));
-        const dim3 g_syn(syn_blocks, (unsigned)tiles);
-        for (int64_t s = 0;; s++) {
+        ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, co};
+        const Refill rfr{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
+                         d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0};
+        int rc = LDPC_OK;
+        for (int64_t s = 0; rc == LDPC_OK; s++) {
             const bool poll = (s % res_poll) == res_poll - 1;
             const int64_t pi = s / res_poll;
             const int slot = (int)(pi % kRing);
-            cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
-            if (poll) LDPC_HIP(hipMemsetAsync(cs.occ_count, 0, sizeof(unsigned long long), stream));
-            if (reg_rowT)
-                LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome_res<72>, g_syn, dim3(256), 0, stream, hard, d_row_ptr,
-                                                 d_col_idx, d_col_idx_T, M, N, max_iter, cs, co, d_unsat, d_done));
-            else
-                LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome_res<0>, g_syn, dim3(256), 0, stream, hard, d_row_ptr,
-                                                 d_col_idx, d_col_idx_T, M, N, max_iter, cs, co, d_unsat, d_done));
+            rs.cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
+            if (poll) LDPC_HIP(hipMemsetAsync(rs.cs.occ_count, 0, sizeof(unsigned long long), stream));
+            rstep = &rs;
+            rc = launch_check(stream, v2c, 0, (unsigned)tiles);
+            rstep = nullptr;
+            if (rc) break;
             if (poll) {
-                LDPC_HIP(hipMemcpyAsync(h_occ + slot, cs.occ_count, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                        stream));
+                LDPC_HIP(hipMemcpyAsync(h_occ + slot, rs.cs.occ_count, sizeof(unsigned long long),
+                                        hipMemcpyDeviceToHost, stream));
                 LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
             }
-            int rc;
-            if ((rc = launch_check(stream, v2c, 0, (unsigned)tiles))) return rc;
-            if ((rc = launch_var(stream, v2c, 0, (unsigned)tiles, pt, rf))) return rc;
+            if ((rc = launch_var(stream, v2c, 0, (unsigned)tiles, pt, rfr))) break;
             if (poll && pi >= kLag) {
                 const int old = (int)((pi - kLag) % kRing);
                 LDPC_HIP(hipEventSynchronize(ev_ring[old]));
                 if (h_occ[old] == 0) break;
             }
         }
-        return LDPC_OK;
+        return rc;
     }
     // While the pool is mostly occupied, launch per tile group (c2v stays in the
     // Infinity Cache); once the input is drained and few lanes remain, one

@@ -45,10 +45,14 @@ struct Engine {
     int full_lanes = 0;       // all lanes of an active tile store (whole cache lines)
     int var_cpw = 1;          // variable phase: columns per wave (k_var_m when > 1)
     bool msa_c = false;       // min-sum with compressed c2v (records + codes, k_check_msa_c / k_var_msa_c)
-    bool res = false;         // resident pool: a few tiles iterated in place (c2v overwrites v2c), k_syndrome_res
+    bool res = false;         // resident pool: a few tiles iterated in place (c2v overwrites v2c), syndrome in the check kernel
     int res_poll = 4;         // res: steps between occupancy polls
     unsigned long long* d_unsat = nullptr;  // res: [tile] syndrome words of the step
-    unsigned int* d_done = nullptr;         // res: [tile] syndrome blocks arrived
+    unsigned int* d_done = nullptr;         // res: [tile] check blocks arrived
+    uint64_t* d_fin = nullptr;              // res: [tile] lanes finished at the step
+    int64_t* d_fin_b = nullptr;             // res: [tile*64] their codeword index
+    int32_t* d_fin_n = nullptr;             // res: [tile*64] their iteration count
+    const dev::ResStep* rstep = nullptr;    // res: set around the check launch of a step
     static constexpr int kRing = 8, kLag = 2;
     uint64_t* d_fresh = nullptr;
     uint64_t* d_occ = nullptr;
@@ -112,6 +116,7 @@ struct Engine {
     int mark_begin(KClass c, hipStream_t s, hipEvent_t* b);
     int mark_end(KClass c, hipStream_t s, hipEvent_t b);
     int probe_c2v(int probes);
+    int probe_res(int probes);
     int launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt);
     int launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt, const dev::Refill& rf);
 };

@@ -14,6 +14,15 @@ struct Refill {
     const int64_t* lane_b;  // [tile*64] codeword index held by each lane
     const double* in;       // [B][N] input (LLR or LR)
     int in_is_llr;
+    // resident pool (engine `res`, k_var_m only): outputs of the codewords
+    // that finished at this step's syndrome, written before their lanes are
+    // refilled (fin == nullptr: the syndrome kernel wrote them)
+    const uint64_t* fin;    // [tile] finished lanes
+    const int64_t* fin_b;   // [tile*64] their codeword index
+    const int32_t* fin_n;   // [tile*64] their iteration count
+    uint8_t* hard_out;      // [B][N]
+    double* post_out;       // [B][N] or nullptr
+    int post_ratio;
 };
 
 struct ContState {
@@ -35,6 +44,22 @@ struct ContOut {
     const double* post_t;  // [tile][N][64] per-iteration posterior (when post)
     const double* prior;   // [tile][N][64]
     int algo_msa, post_ratio;
+};
+
+// Resident pool: the syndrome of the previous variable phase is computed by
+// the check kernel (each wave its row's parity) and the last block of a tile
+// to finish runs the lane bookkeeping (k_check_bp / k_check_msa with SYN).
+struct ResStep {
+    const uint64_t* hard;        // [tile][N] ballots
+    const int32_t* col_idx;      // [E] CSR column of each edge (regular rows)
+    unsigned long long* unsat;   // [tile] OR of the row parities (re-armed by the last block)
+    unsigned int* done;          // [tile] blocks arrived (re-armed by the last block)
+    uint64_t* fin;               // [tile] lanes finished at this step -> Refill::fin
+    int64_t* fin_b;              // [tile*64]
+    int32_t* fin_n;              // [tile*64]
+    int32_t N, max_iter;
+    ContState cs;
+    ContOut co;                  // iters / valid (hard / post are written by k_var_m)
 };
 
 }  // namespace dev

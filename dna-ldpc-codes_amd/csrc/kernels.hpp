@@ -73,6 +73,140 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
     return x ^ (x >> 31);
 }
 
+// Lane bookkeeping of tile t once its syndrome word U is known (threads 0..63
+// of the block; lane = threadIdx.x).  Shared with k_syndrome_res.
+// ln0 / b0: the lane's cs.lane_n / cs.lane_b, loaded by the caller (only
+// meaningful for occupied lanes).  probe: read the claim counter before
+// claiming (avoids atomics on it once the input is exhausted).
+__device__ __forceinline__ void cont_lanes(int64_t t, uint64_t occ, uint64_t U, int32_t max_iter, const ContState& cs,
+                                           const ContOut& co, int64_t* s_b, int32_t* s_n, uint64_t* s_fin,
+                                           int32_t ln0, int64_t b0, bool probe)
+{
+    const int lane = lane_id();
+    {
+        const size_t li = (size_t)t * TILE + lane;
+        const bool o = (occ >> lane) & 1ull;
+        const int32_t ln = o ? ln0 : 0;
+        const bool unsat = (U >> lane) & 1ull;
+        const bool fin = o && (!unsat || ln == max_iter);
+        const bool cont = o && !fin;
+        const int64_t b = o ? b0 : -1;
+        if (fin) { co.iters[b] = ln; co.valid[b] = unsat ? 0 : 1; }
+        s_b[lane] = b;
+        s_n[lane] = ln;
+        const uint64_t F = __ballot(fin), Cm = __ballot(cont);
+        // refill every lane that is not continuing
+        const uint64_t freem = ~Cm;
+        const int nfree = __popcll(freem);
+        unsigned long long base = 0;
+        if (lane == 0 && nfree > 0) {
+            if (probe) {
+                const unsigned long long nb = __hip_atomic_load(cs.next_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                base = (nb < (unsigned long long)cs.B) ? atomicAdd(cs.next_b, (unsigned long long)nfree) : nb;
+            } else {
+                base = atomicAdd(cs.next_b, (unsigned long long)nfree);
+            }
+        }
+        base = __shfl(base, 0);
+        const int rank = __popcll(freem & ((1ull << lane) - 1ull));
+        const bool fresh = !cont && (base + (unsigned long long)rank < (unsigned long long)cs.B);
+        const uint64_t Fr = __ballot(fresh);
+        if (cont) cs.lane_n[li] = ln + 1;
+        if (fresh) { cs.lane_b[li] = (int64_t)(base + rank); cs.lane_n[li] = 0; }
+        if (lane == 0) {
+            cs.active[t] = Cm;
+            cs.fresh[t] = Fr;
+            cs.occupied[t] = Cm | Fr;
+            *s_fin = F;
+            if ((Cm | Fr) && cs.occ_count) atomicAdd(cs.occ_count, (unsigned long long)__popcll(Cm | Fr));
+        }
+    }
+}
+
+// The finished codewords' outputs (hard bits of this step, posterior), all
+// threads of the block.
+__device__ __forceinline__ void cont_outputs(int64_t t, uint64_t F, const uint64_t* __restrict__ h, int32_t N,
+                                             const ContOut& co, const int64_t* s_b, const int32_t* s_n)
+{
+    for (int32_t j = threadIdx.x; j < N; j += blockDim.x) {
+        const uint64_t wj = h[j];
+        for (uint64_t f = F; f; f &= f - 1) {
+            const int l = __builtin_ctzll(f);
+            const size_t ob = (size_t)s_b[l] * N + j;
+            co.hard[ob] = (uint8_t)((wj >> l) & 1ull);
+            if (co.post) {
+                const size_t pj = ((size_t)t * N + j) * TILE + l;
+                const double pv = s_n[l] > 0 ? co.post_t[pj] : co.prior[pj];
+                if (co.algo_msa) co.post[ob] = pv;
+                else {
+                    const double P = __builtin_isnan(pv) ? 1.0 : pv;
+                    co.post[ob] = co.post_ratio ? P : log(P);
+                }
+            }
+        }
+    }
+}
+
+// Resident pool (ResStep): the parity of one row over the ballots of the
+// previous variable phase, one gathered ballot per lane (DC / 64 rounds)
+// and an XOR across the wave; the result is wave-uniform.
+template <int DC>
+__device__ __forceinline__ uint64_t row_parity(const uint64_t* __restrict__ h, const int32_t* __restrict__ cols)
+{
+    const int lane = lane_id();
+    uint64_t p = 0;
+#pragma unroll
+    for (int k0 = 0; k0 < DC; k0 += TILE)
+        if (k0 + lane < DC) p ^= h[cols[k0 + lane]];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) p ^= shfl_xor_u64(p, off);
+    return p;
+}
+
+// Resident pool epilogue of a check block (all 256 threads): OR the block's
+// row parities into unsat[t]; the last block of the tile to arrive runs the
+// lane bookkeeping for the step (cont_lanes: iters / valid, refill claims,
+// active / fresh / occupied masks) and hands the finished lanes to the
+// variable kernel, which writes their outputs before refilling them.
+__device__ __forceinline__ void res_arrive(int64_t t, uint64_t occ, uint64_t p, const ResStep& rs, int32_t ln0,
+                                           int64_t b0)
+{
+    __shared__ uint64_t red[4];
+    __shared__ int64_t s_b[TILE];
+    __shared__ int32_t s_n[TILE];
+    __shared__ uint64_t s_fin;
+    __shared__ int s_last;
+    const int lane = lane_id(), w = wave_id();
+    if (lane == 0) red[w] = p;
+    __syncthreads();
+    // No fences: an agent-scope release would write back the L2 in every
+    // block.  Only device-coherent atomics carry data between the blocks; the
+    // arrival is issued after the OR has returned (its value is consumed), and
+    // the last block reads the word back with an RMW.  Everything else the
+    // bookkeeping reads was written by earlier kernels.
+    if (threadIdx.x == 0) {
+        const uint64_t U = red[0] | red[1] | red[2] | red[3];
+        unsigned long long o = 0;
+        if (U) o = atomicOr(rs.unsat + t, (unsigned long long)U);
+        asm volatile("" ::"v"(o) : "memory");
+        s_last = atomicAdd(rs.done + t, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x < TILE) {
+        const uint64_t U = occ ? (uint64_t)atomicOr(rs.unsat + t, 0ull) : 0ull;
+        cont_lanes(t, occ, U, rs.max_iter, rs.cs, rs.co, s_b, s_n, &s_fin, ln0, b0, false);
+        const size_t li = (size_t)t * TILE + lane;
+        rs.fin_b[li] = s_b[lane];
+        rs.fin_n[li] = s_n[lane];
+        if (lane == 0) {
+            rs.fin[t] = s_fin;
+            atomicExch(rs.unsat + t, 0ull);
+            atomicExch(rs.done + t, 0u);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // init: transpose a [b][N] input chunk into the tiled layout, set the initial
 // messages and hard decisions.
@@ -190,28 +324,14 @@ __global__ __launch_bounds__(1024) void k_syndrome(const uint64_t* __restrict__ 
 // -> identical values), which keeps the kernel at 2 waves/SIMD.
 // grid (ceil(M/4), tiles), block 256: one wave per (row, tile).
 // ---------------------------------------------------------------------------
+// c2v scratch: CSR order (row-contiguous) or CSC order (column-contiguous,
+// position pos[e]) so the variable phase reads each column contiguously
 template <int DC, bool NT, bool CSCL>
-__global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ dmsg, double* __restrict__ lr,
-                                                     const uint64_t* __restrict__ active,
-                                                     const int32_t* __restrict__ pos, int32_t M, int64_t E,
-                                                     int64_t t0, int full_lanes)
+__device__ __forceinline__ void check_bp_row(const double* __restrict__ src, double* __restrict__ dst,
+                                             const int32_t* __restrict__ prow, int32_t row)
 {
     constexpr int SEG = 8;
     constexpr int NSEG = (DC + SEG - 1) / SEG;
-    const int lane = lane_id();
-    const int32_t row = blockIdx.x * 4 + wave_id();
-    const int64_t t = t0 + blockIdx.y;
-    if (row >= M) return;
-    const uint64_t act = active[t];
-    // full_lanes: converged / empty lanes of an active tile run along on their
-    // stale state so every c2v store covers whole lines (their values are never read)
-    if ((full_lanes & 1) ? act == 0 : !((act >> lane) & 1ull)) return;
-    const double* __restrict__ src = dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
-    // c2v scratch: CSR order (row-contiguous) or CSC order (column-contiguous,
-    // position pos[e]) so the variable phase reads each column contiguously
-    double* __restrict__ dst = lr + (size_t)blockIdx.y * E * TILE + lane;
-    const int32_t* __restrict__ prow = pos + (size_t)row * DC;
-
     double x[DC];
 #pragma unroll
     for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
@@ -247,6 +367,43 @@ __global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ 
             }
         }
     }
+}
+
+// SYN (resident pool, ResStep): the lanes run are the tile's occupied ones,
+// every wave also takes its row's parity over the previous variable phase's
+// ballots, and every block ends in res_arrive (no early exit).
+template <int DC, bool NT, bool CSCL, bool SYN>
+__global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ dmsg, double* __restrict__ lr,
+                                                     const uint64_t* __restrict__ active,
+                                                     const int32_t* __restrict__ pos, int32_t M, int64_t E,
+                                                     int64_t t0, int full_lanes, ResStep rs)
+{
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = t0 + blockIdx.y;
+    const uint64_t act = SYN ? rs.cs.occupied[t] : active[t];
+    // full_lanes: converged / empty lanes of an active tile run along on their
+    // stale state so every c2v store covers whole lines (their values are never read)
+    const bool run = row < M && ((full_lanes & 1) ? act != 0 : ((act >> lane) & 1ull));
+    if constexpr (!SYN) {
+        if (!run) return;
+    }
+    uint64_t par = 0;
+    int32_t ln0 = 0;
+    int64_t b0 = 0;
+    if (SYN && act != 0) {
+        // the lane state for res_arrive's bookkeeping (used by the tile's last
+        // block only), loaded up front so it is not on the tail's chain
+        if (threadIdx.x < TILE && ((act >> lane) & 1ull)) {
+            ln0 = rs.cs.lane_n[t * TILE + lane];
+            b0 = rs.cs.lane_b[t * TILE + lane];
+        }
+        if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
+    }
+    if (run)
+        check_bp_row<DC, NT, CSCL>(dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane,
+                                   lr + (size_t)blockIdx.y * E * TILE + lane, pos + (size_t)row * DC, row);
+    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0);
 }
 
 // Generic row degree: the prefix products go through the lr array exactly as
@@ -370,9 +527,19 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
     const uint64_t act = active[t];
     const uint64_t frm = CONT ? rf.fresh[t] : 0ull;
     const uint64_t touched = act | frm;
-    if (touched == 0) return;
+    // resident pool: lanes whose codeword finished at this step's syndrome
+    // (their outputs are written here, before a refill overwrites the lane)
+    const uint64_t fm = (CONT && rf.fin) ? rf.fin[t] : 0ull;
+    if (touched == 0 && fm == 0) return;
     const bool live = (act >> lane) & 1ull;
     const bool fr = CONT && ((frm >> lane) & 1ull);
+    const bool fl = (fm >> lane) & 1ull;
+    int64_t fb = 0;
+    int32_t fn = 0;
+    if (fl) {
+        fb = rf.fin_b[t * TILE + lane];
+        fn = rf.fin_n[t * TILE + lane];
+    }
     const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
     int32_t eid[CPW][DV];
 #pragma unroll
@@ -399,6 +566,21 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
     for (int c = 0; c < CPW; ++c) {
         const int32_t j = j0 + c;
         const size_t pj = ((size_t)t * N + j) * TILE + lane;
+        if (CONT && fm != 0ull) {  // finished codeword: hard bit (+ posterior) of its exit
+            const uint64_t hw = hard[(size_t)t * N + j];
+            if (fl) {
+                const size_t ob = (size_t)fb * N + j;
+                rf.hard_out[ob] = (uint8_t)((hw >> lane) & 1ull);
+                if (rf.post_out) {
+                    const double pv = fn > 0 ? post[pj] : prior[pj];
+                    if (MSA) rf.post_out[ob] = pv;
+                    else {
+                        const double P = __builtin_isnan(pv) ? 1.0 : pv;
+                        rf.post_out[ob] = rf.post_ratio ? P : log(P);
+                    }
+                }
+            }
+        }
         bool h = false;
         double dv[DV];
 #pragma unroll
@@ -528,26 +710,13 @@ __global__ __launch_bounds__(256) void k_var_bp_gen(const double* __restrict__ l
 // dc == 1: mag stays -1 -> 0, sign 1 -> 0.0 (dec.cpp:1427-1430).
 // ---------------------------------------------------------------------------
 template <int DC, bool NT, bool CSCL>
-__global__ __launch_bounds__(256) void k_check_msa(const double* __restrict__ v2c, double* __restrict__ c2v,
-                                                   const uint64_t* __restrict__ active,
-                                                   const int32_t* __restrict__ pos, int32_t M, int64_t E,
-                                                   int64_t t0, int full_lanes)
+__device__ __forceinline__ void check_msa_row(const double* __restrict__ src, double* __restrict__ dst,
+                                              const int32_t* __restrict__ prow, int32_t row)
 {
-    const int lane = lane_id();
-    const int32_t row = blockIdx.x * 4 + wave_id();
-    const int64_t t = t0 + blockIdx.y;
-    if (row >= M) return;
-    const uint64_t act = active[t];
-    // full_lanes: converged / empty lanes of an active tile run along on their
-    // stale state so every c2v store covers whole lines (their values are never read)
-    if ((full_lanes & 1) ? act == 0 : !((act >> lane) & 1ull)) return;
-    const double* __restrict__ src = v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
-    double* __restrict__ dst = c2v + (size_t)blockIdx.y * E * TILE + lane;
-    const int32_t* __restrict__ prow = pos + (size_t)row * DC;
     double x[DC];
 #pragma unroll
     for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
-    if (DC == 1) {
+    if constexpr (DC == 1) {
         dst[(CSCL ? (size_t)prow[0] : (size_t)row) * TILE] = 0.0;
         return;
     }
@@ -576,6 +745,40 @@ __global__ __launch_bounds__(256) void k_check_msa(const double* __restrict__ v2
         const size_t p = CSCL ? (size_t)prow[k] : (size_t)row * DC + k;
         dst[p * TILE] = (double)sign * mag;
     }
+}
+
+template <int DC, bool NT, bool CSCL, bool SYN>
+__global__ __launch_bounds__(256) void k_check_msa(const double* __restrict__ v2c, double* __restrict__ c2v,
+                                                   const uint64_t* __restrict__ active,
+                                                   const int32_t* __restrict__ pos, int32_t M, int64_t E,
+                                                   int64_t t0, int full_lanes, ResStep rs)
+{
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = t0 + blockIdx.y;
+    const uint64_t act = SYN ? rs.cs.occupied[t] : active[t];
+    // full_lanes: converged / empty lanes of an active tile run along on their
+    // stale state so every c2v store covers whole lines (their values are never read)
+    const bool run = row < M && ((full_lanes & 1) ? act != 0 : ((act >> lane) & 1ull));
+    if constexpr (!SYN) {
+        if (!run) return;
+    }
+    uint64_t par = 0;
+    int32_t ln0 = 0;
+    int64_t b0 = 0;
+    if (SYN && act != 0) {
+        // the lane state for res_arrive's bookkeeping (used by the tile's last
+        // block only), loaded up front so it is not on the tail's chain
+        if (threadIdx.x < TILE && ((act >> lane) & 1ull)) {
+            ln0 = rs.cs.lane_n[t * TILE + lane];
+            b0 = rs.cs.lane_b[t * TILE + lane];
+        }
+        if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
+    }
+    if (run)
+        check_msa_row<DC, NT, CSCL>(v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane,
+                                    c2v + (size_t)blockIdx.y * E * TILE + lane, pos + (size_t)row * DC, row);
+    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0);
 }
 
 __global__ __launch_bounds__(256) void k_check_msa_gen(const double* __restrict__ v2c, double* __restrict__ c2v,
@@ -979,72 +1182,6 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ pos
 // Which lane decodes which codeword varies run to run; each codeword's
 // arithmetic does not.
 // ---------------------------------------------------------------------------
-// Lane bookkeeping of tile t once its syndrome word U is known (threads 0..63
-// of the block; lane = threadIdx.x).  Shared with k_syndrome_res.
-__device__ __forceinline__ void cont_lanes(int64_t t, uint64_t occ, uint64_t U, int32_t max_iter, const ContState& cs,
-                                           const ContOut& co, int64_t* s_b, int32_t* s_n, uint64_t* s_fin)
-{
-    const int lane = lane_id();
-    {
-        const size_t li = (size_t)t * TILE + lane;
-        const bool o = (occ >> lane) & 1ull;
-        const int32_t ln = o ? cs.lane_n[li] : 0;
-        const bool unsat = (U >> lane) & 1ull;
-        const bool fin = o && (!unsat || ln == max_iter);
-        const bool cont = o && !fin;
-        const int64_t b = o ? cs.lane_b[li] : -1;
-        if (fin) { co.iters[b] = ln; co.valid[b] = unsat ? 0 : 1; }
-        s_b[lane] = b;
-        s_n[lane] = ln;
-        const uint64_t F = __ballot(fin), Cm = __ballot(cont);
-        // refill every lane that is not continuing
-        const uint64_t freem = ~Cm;
-        const int nfree = __popcll(freem);
-        unsigned long long base = 0;
-        if (lane == 0) {
-            const unsigned long long nb = __hip_atomic_load(cs.next_b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            base = (nb < (unsigned long long)cs.B) ? atomicAdd(cs.next_b, (unsigned long long)nfree) : nb;
-        }
-        base = __shfl(base, 0);
-        const int rank = __popcll(freem & ((1ull << lane) - 1ull));
-        const bool fresh = !cont && (base + (unsigned long long)rank < (unsigned long long)cs.B);
-        const uint64_t Fr = __ballot(fresh);
-        if (cont) cs.lane_n[li] = ln + 1;
-        if (fresh) { cs.lane_b[li] = (int64_t)(base + rank); cs.lane_n[li] = 0; }
-        if (lane == 0) {
-            cs.active[t] = Cm;
-            cs.fresh[t] = Fr;
-            cs.occupied[t] = Cm | Fr;
-            *s_fin = F;
-            if ((Cm | Fr) && cs.occ_count) atomicAdd(cs.occ_count, (unsigned long long)__popcll(Cm | Fr));
-        }
-    }
-}
-
-// The finished codewords' outputs (hard bits of this step, posterior), all
-// threads of the block.
-__device__ __forceinline__ void cont_outputs(int64_t t, uint64_t F, const uint64_t* __restrict__ h, int32_t N,
-                                             const ContOut& co, const int64_t* s_b, const int32_t* s_n)
-{
-    for (int32_t j = threadIdx.x; j < N; j += blockDim.x) {
-        const uint64_t wj = h[j];
-        for (uint64_t f = F; f; f &= f - 1) {
-            const int l = __builtin_ctzll(f);
-            const size_t ob = (size_t)s_b[l] * N + j;
-            co.hard[ob] = (uint8_t)((wj >> l) & 1ull);
-            if (co.post) {
-                const size_t pj = ((size_t)t * N + j) * TILE + l;
-                const double pv = s_n[l] > 0 ? co.post_t[pj] : co.prior[pj];
-                if (co.algo_msa) co.post[ob] = pv;
-                else {
-                    const double P = __builtin_isnan(pv) ? 1.0 : pv;
-                    co.post[ob] = co.post_ratio ? P : log(P);
-                }
-            }
-        }
-    }
-}
-
 // one block per tile
 template <int DC>
 __global__ __launch_bounds__(1024) void k_syndrome_cont(const uint64_t* __restrict__ hard,
@@ -1082,80 +1219,9 @@ __global__ __launch_bounds__(1024) void k_syndrome_cont(const uint64_t* __restri
         uint64_t U = 0;
         if (occ)
             for (int q = 0; q < (int)(blockDim.x >> 6); ++q) U |= red[q];
-        cont_lanes(t, occ, U, max_iter, cs, co, s_b, s_n, &s_fin);
-    }
-    __syncthreads();
-    if (s_fin) cont_outputs(t, s_fin, h, N, co, s_b, s_n);
-}
-
-// ---------------------------------------------------------------------------
-// Resident-pool syndrome step (engine `res` mode: a pool of a few tiles,
-// iterated in place).  One block per tile would leave a 2-tile pool's
-// syndrome a long serial chain, so a tile's rows are spread over gridDim.x
-// blocks (two threads per row, DC/2 gathers each); every block ORs its
-// parities into unsat[t], and the last block of the tile to arrive (counter
-// done[t]) runs the lane bookkeeping and output writes of k_syndrome_cont,
-// then re-arms unsat[t] / done[t] for the next step.  grid (blocks, tiles),
-// block 256.
-// ---------------------------------------------------------------------------
-template <int DC>
-__global__ __launch_bounds__(256) void k_syndrome_res(const uint64_t* __restrict__ hard,
-                                                      const int32_t* __restrict__ row_ptr,
-                                                      const int32_t* __restrict__ col_idx,
-                                                      const int32_t* __restrict__ col_idx_T, int32_t M, int32_t N,
-                                                      int32_t max_iter, ContState cs, ContOut co,
-                                                      unsigned long long* __restrict__ unsat,
-                                                      unsigned int* __restrict__ done)
-{
-    __shared__ uint64_t red[4];
-    __shared__ int64_t s_b[TILE];
-    __shared__ int32_t s_n[TILE];
-    __shared__ uint64_t s_fin;
-    __shared__ int s_last;
-    const int64_t t = blockIdx.y;
-    const uint64_t occ = cs.occupied[t];
-    const int lane = lane_id(), w = wave_id();
-    const uint64_t* h = hard + (size_t)t * N;
-    uint64_t u = 0;
-    if (occ) {
-        const int half = threadIdx.x & 1;
-        for (int32_t i = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 1); i < M;
-             i += (int32_t)((gridDim.x * blockDim.x) >> 1)) {
-            uint64_t p = 0;
-            if (DC > 0) {
-                constexpr int H = (DC + 1) / 2;
-                const int k0 = half * H;
-#pragma unroll
-                for (int k = 0; k < H; ++k)
-                    if (k0 + k < DC) p ^= h[col_idx_T[(size_t)(k0 + k) * M + i]];
-            } else {
-                for (int32_t e = row_ptr[i] + half; e < row_ptr[i + 1]; e += 2) p ^= h[col_idx[e]];
-            }
-            p ^= shfl_xor_u64(p, 1);  // the row's parity: XOR of both halves
-            u |= p;
-        }
-#pragma unroll
-        for (int off = 32; off > 1; off >>= 1) u |= shfl_xor_u64(u, off);
-    }
-    if (lane == 0) red[w] = u;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t U = 0;
-        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) U |= red[q];
-        if (U) atomicOr(unsat + t, (unsigned long long)U);
-        __threadfence();
-        s_last = atomicAdd(done + t, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    if (threadIdx.x < 64) {
-        const uint64_t U = __hip_atomic_load(unsat + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        cont_lanes(t, occ, occ ? U : 0ull, max_iter, cs, co, s_b, s_n, &s_fin);
-        if (threadIdx.x == 0) {
-            __hip_atomic_store(unsat + t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(done + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        const size_t li = (size_t)t * TILE + lane;
+        const bool o = (occ >> lane) & 1ull;
+        cont_lanes(t, occ, U, max_iter, cs, co, s_b, s_n, &s_fin, o ? cs.lane_n[li] : 0, o ? cs.lane_b[li] : -1, true);
     }
     __syncthreads();
     if (s_fin) cont_outputs(t, s_fin, h, N, co, s_b, s_n);

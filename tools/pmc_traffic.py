@@ -22,6 +22,8 @@ CLASSES = {  # logical class -> kernel-name prefixes (template instantiations)
     "k_var_bp": ("ldpc::dev::k_var_m<false", "ldpc::dev::k_var_bp<"),
     "k_check_msa": ("ldpc::dev::k_check_msa<",),
     "k_var_msa": ("ldpc::dev::k_var_m<true", "ldpc::dev::k_var_msa<"),
+    "k_check_msa_c": ("ldpc::dev::k_check_msa_c<",),
+    "k_var_msa_c": ("ldpc::dev::k_var_msa_c<",),
 }
 
 
