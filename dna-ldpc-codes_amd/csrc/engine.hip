@@ -769,10 +769,13 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, co};
         const Refill rfr{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
                          d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0};
+        // batches of a few pool fills (the DNA batch) poll every step: the
+        // host stops at most kLag steps after the pool empties
+        const int every = B <= 8 * cap ? 1 : res_poll;
         int rc = LDPC_OK;
         for (int64_t s = 0; rc == LDPC_OK; s++) {
-            const bool poll = (s % res_poll) == res_poll - 1;
-            const int64_t pi = s / res_poll;
+            const bool poll = (s % every) == every - 1;
+            const int64_t pi = s / every;
             const int slot = (int)(pi % kRing);
             rs.cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
             if (poll) LDPC_HIP(hipMemsetAsync(rs.cs.occ_count, 0, sizeof(unsigned long long), stream));

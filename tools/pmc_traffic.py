@@ -3,7 +3,12 @@
 the rocprofv3 PMC passes of tools/gpu_profile.sh, written as the
 pmc_traffic.json bench.py reads for the roofline `traffic` field.
 
-    python tools/pmc_traffic.py gpurun_out/<tag> <cw_iters> profiles/<round>/pmc_traffic.json
+    python tools/pmc_traffic.py gpurun_out/<tag> <cw_iters> profiles/<round>/pmc_traffic.json [exclude ...]
+
+exclude: kernel names to leave out (e.g. the engine's placement-probe
+launches, which run outside the decode: the plain in-place instantiations
+k_check_bp<72;false;false;false> / k_var_m<false;8;false;false;4> of the
+resident pool).
 
 cw_iters = executed codeword-iterations of the profiled run (the PMC passes
 run bench.py --batch-per-gpu 1024 on BSC p=0.02, which never converges: 1024
@@ -29,12 +34,13 @@ CLASSES = {  # logical class -> kernel-name prefixes (template instantiations)
 
 def main():
     d, cw_iters, out = sys.argv[1], float(sys.argv[2]), sys.argv[3]
+    exclude = set(sys.argv[4:])
     agg = pmc_summary.load(d)
     per, kernels = {}, {}
     for cls, prefixes in CLASSES.items():
         tot, names = 0.0, []
         for k, cs in agg.items():
-            if not k.startswith(prefixes):
+            if not k.startswith(prefixes) or k in exclude:
                 continue
             names.append(k)
             for c, mult in (("FETCH_SIZE", 2048.0), ("WRITE_SIZE", 1024.0)):
