@@ -277,7 +277,7 @@ def main():
                    "algo": algo, "parallelism": f"dp{world} (contiguous codeword shards, no collective)",
                    "resident_per_pass": eng.cap, "group_tiles": eng.group_tiles, "nontemporal_d": eng.nontemporal,
                    "two_stream": eng.pipeline, "continuous": eng.continuous, "resident_pool": eng.resident,
-                   "compressed_msa": eng.msa_compressed,
+                   "compressed_msa": eng.msa_compressed, "syndrome_split": eng.syndrome_split,
                    "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 4)},
         "roofline": roof,
     }

@@ -44,7 +44,11 @@ constexpr int64_t kDefaultMsaC = 1;  // LDPC_MSA_C: compressed min-sum c2v (tool
 constexpr int64_t kDefaultVarCpw = 4;  // LDPC_VAR_CPW (A/B over two boxes: +2.6-2.9% over 1 column per wave)
 constexpr int64_t kDefaultRes = 1;       // LDPC_RES: resident in-place pool for BP / fp64 min-sum in continuous mode
 constexpr int64_t kDefaultResTiles = 3;  // LDPC_RES_TILES: pool tiles (3 x 85 MB ~ the 256 MB Infinity Cache; A/B)
-constexpr int64_t kDefaultResPoll = 8;   // LDPC_RES_POLL: steps between occupancy polls
+constexpr int64_t kDefaultResPoll = 8;
+constexpr int64_t kDefaultSynSplit = 32;     // LDPC_SYN_SPLIT: syndrome blocks per tile in continuous mode (0: one block, k_syndrome_cont; A/B min-sum config 5 +5-6 %)
+constexpr int64_t kDefaultSynFused = 0;      // LDPC_SYN_FUSED: grouped continuous mode, syndrome fused into the check kernel
+constexpr int64_t kDefaultResMsaC = 0;       // LDPC_RES_MSA_C: resident pool for compressed min-sum
+constexpr int64_t kDefaultResTilesMsaC = 2;  // LDPC_RES_TILES_MSA_C: its pool tiles   // LDPC_RES_POLL: steps between occupancy polls
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
@@ -120,8 +124,10 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     // Infinity Cache, check->variable messages written over the variable->check
     // messages they are computed from (each row's / column's edges are read
     // into registers before its outputs are stored), no c2v scratch
-    if (res_mode < 0) res_mode = (int)env_int("LDPC_RES", kDefaultRes);
-    res = res_mode != 0 && cont && !msa_c && g->N % 32 == 0;  // k_var_m at any columns-per-wave
+    // (compressed min-sum: its own switch, LDPC_RES_MSA_C; k_var_msa_c needs N % 16)
+    if (res_mode < 0)
+        res_mode = (int)(msa_c ? env_int("LDPC_RES_MSA_C", kDefaultResMsaC) : env_int("LDPC_RES", kDefaultRes));
+    res = res_mode != 0 && cont && (msa_c ? g->N % 16 == 0 : g->N % 32 == 0);  // k_var_m at any columns-per-wave
     if (res) {
         nt = 0;  // the pool is meant to stay cached
         pipelined = 0;
@@ -134,7 +140,8 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         // half of the free memory for the resident state, at most 16384 codewords;
         // compressed min-sum in continuous mode: a small lane pool (its scattered
         // v2c stores run ~45 % longer over a 19 GB pool than over 1.2 GB, A/B)
-        const int64_t want = res ? 64 * env_int("LDPC_RES_TILES", kDefaultResTiles)
+        const int64_t want = res ? 64 * (msa_c ? env_int("LDPC_RES_TILES_MSA_C", kDefaultResTilesMsaC)
+                                             : env_int("LDPC_RES_TILES", kDefaultResTiles))
                              : (msa_c && cont) ? env_int("LDPC_MSA_POOL", kDefaultMsaPool) : 16384;
         chunk = std::min<int64_t>(want, (int64_t)(fr / 2) / engine_bytes_per_codeword(*g));
     }
@@ -193,17 +200,30 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     }
     if (csc < 0) csc = (int)env_int("LDPC_LR_CSC", kDefaultCsc);
     lr_csc = csc != 0 && g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
+    // grouped continuous mode with the resident pool's fused syndrome step:
+    // check(group) runs the syndrome + lane bookkeeping of its tiles (ResStep),
+    // variable(group) writes the finished lanes' outputs (k_var_m / k_var_msa_c)
+    syn_fused = cont && !res && !pipe && !lr_csc && g->N % 32 == 0 && env_int("LDPC_SYN_FUSED", kDefaultSynFused) != 0;
+    // or a separate syndrome launch spread over several blocks per tile, same hand-off
+    syn_split = (cont && !res && !syn_fused && !pipe && !lr_csc && g->N % 32 == 0)
+                    ? (int)std::max<int64_t>(0, std::min<int64_t>(env_int("LDPC_SYN_SPLIT", kDefaultSynSplit), 256))
+                    : 0;
     const size_t E = (size_t)std::max<int64_t>(g->E, 1);
     LDPC_HIP(hipMalloc((void**)&v2c, (size_t)cap * E * sizeof(double)));
     // continuous mode's drain tail (< 1/32 occupancy) launches wider groups
-    if (res) {
-        c2v_tiles = cap_tiles;
-        c2v = v2c;  // in place
+    if (res || syn_fused || syn_split) {
         LDPC_HIP(hipMalloc((void**)&d_unsat, (size_t)cap_tiles * sizeof(unsigned long long)));
         LDPC_HIP(hipMalloc((void**)&d_done, (size_t)cap_tiles * sizeof(unsigned int)));
         LDPC_HIP(hipMalloc((void**)&d_fin, (size_t)cap_tiles * sizeof(uint64_t)));
         LDPC_HIP(hipMalloc((void**)&d_fin_b, (size_t)cap * sizeof(int64_t)));
         LDPC_HIP(hipMalloc((void**)&d_fin_n, (size_t)cap * sizeof(int32_t)));
+    }
+    if (res) {
+        c2v_tiles = cap_tiles;
+        if (msa_c)  // codes + records of the whole pool (13.6 MB per tile for the DNA code)
+            LDPC_HIP(hipMalloc((void**)&c2v, (size_t)cap_tiles * 64 * (E + (size_t)g->M * dev::MSA_REC_PLANES * 8)));
+        else
+            c2v = v2c;  // in place
     } else {
         c2v_tiles = std::max<int64_t>((pipe ? 2 : 1) * group_tiles, cont ? (cap_tiles + 3) / 4 : 0);
         LDPC_HIP(hipMalloc((void**)&c2v, (size_t)c2v_tiles * 64 * E * sizeof(double)));
@@ -246,11 +266,12 @@ int Engine::probe_res(int probes)
     float best_ms = 1e30f;
     int rc = LDPC_OK;
     for (size_t c = 0; c < cand.size() && rc == LDPC_OK; c++) {
-        v2c = c2v = cand[c];
+        v2c = cand[c];
+        if (!msa_c) c2v = v2c;
         for (int rep = 0; rep < 5 && rc == LDPC_OK; rep++) {  // rep 0 warms up
             if (rep == 1 && hipEventRecord(e0, stream) != hipSuccess) rc = LDPC_ERR_DEVICE;
-            if (!rc) rc = launch_check(stream, v2c, 0, gt);  // rstep == nullptr: plain in-place check
-            if (!rc) rc = launch_var(stream, v2c, 0, gt, nullptr, dev::Refill{});
+            if (!rc) rc = launch_check(stream, c2v, 0, gt);  // rstep == nullptr: plain (in-place) check
+            if (!rc) rc = launch_var(stream, c2v, 0, gt, nullptr, dev::Refill{});
         }
         if (rc) break;
         LDPC_HIP(hipEventRecord(e1, stream));
@@ -264,7 +285,8 @@ int Engine::probe_res(int probes)
     hipEventDestroy(e1);
     for (size_t c = 0; c < cand.size(); c++)
         if (c != best) (void)hipFree(cand[c]);
-    v2c = c2v = cand[best];
+    v2c = cand[best];
+    if (!msa_c) c2v = v2c;
     for (int k = 0; k < K_NCLASS; k++) launches[k] = 0;
     return rc;
 }
@@ -465,7 +487,7 @@ static double* msa_rec(double* scratch, int64_t tiles, int64_t E)
     return reinterpret_cast<double*>(reinterpret_cast<uint8_t*>(scratch) + (size_t)tiles * E * 64);
 }
 
-template <int CPW>
+template <bool NT, int CPW>
 static void var_msa_c(hipStream_t s, unsigned nb, const uint8_t* codes, const double* rec, double* v2c, double* prior,
                       uint64_t* hard, const uint64_t* active, const int32_t* col_edge, const int32_t* col_row,
                       double* pt, int32_t N, int32_t M, int64_t E, int64_t t0, unsigned gt, const dev::Refill& rf,
@@ -473,10 +495,10 @@ static void var_msa_c(hipStream_t s, unsigned nb, const uint8_t* codes, const do
 {
     using namespace dev;
     if (rf.fresh)
-        hipLaunchKernelGGL((k_var_msa_c<8, true, true, CPW>), dim3(nb), dim3(256), 0, s, codes, rec, v2c, prior, hard,
+        hipLaunchKernelGGL((k_var_msa_c<8, NT, true, CPW>), dim3(nb), dim3(256), 0, s, codes, rec, v2c, prior, hard,
                            active, col_edge, col_row, pt, N, M, E, t0, (uint32_t)gt, rf, full);
     else
-        hipLaunchKernelGGL((k_var_msa_c<8, true, false, CPW>), dim3(nb), dim3(256), 0, s, codes, rec, v2c, prior, hard,
+        hipLaunchKernelGGL((k_var_msa_c<8, NT, false, CPW>), dim3(nb), dim3(256), 0, s, codes, rec, v2c, prior, hard,
                            active, col_edge, col_row, pt, N, M, E, t0, (uint32_t)gt, rf, full);
 }
 
@@ -487,8 +509,16 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
     const int64_t E = g->E;
     const bool reg72 = g->regular_dc && g->dc_max == 72;
     const dim3 grid((M + 3) / 4, gt), blk(256);
-    if (res && rstep) {  // resident pool: syndrome + lane bookkeeping fused (ResStep)
-        if (algo == LDPC_ALGO_BP)
+    if ((res || syn_fused) && rstep) {  // syndrome + lane bookkeeping fused (ResStep)
+        if (msa_c && nt_d)
+            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa_c<72, true, true>), grid, blk, 0, s, v2c,
+                                                     msa_codes(scratch), msa_rec(scratch, c2v_tiles, E), active, M, E,
+                                                     t0, full_lanes, *rstep));
+        else if (msa_c)
+            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa_c<72, false, true>), grid, blk, 0, s, v2c,
+                                                     msa_codes(scratch), msa_rec(scratch, c2v_tiles, E), active, M, E,
+                                                     t0, full_lanes, *rstep));
+        else if (algo == LDPC_ALGO_BP)
             LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_bp<72, false, false, true>), grid, blk, 0, s, v2c, scratch,
                                                      active, d_csc_pos, M, E, t0, full_lanes, *rstep));
         else
@@ -497,8 +527,14 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
         return LDPC_OK;
     }
     if (msa_c) {
-        LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa_c<72, true>), grid, blk, 0, s, v2c, msa_codes(scratch),
-                                                 msa_rec(scratch, c2v_tiles, E), active, M, E, t0, full_lanes));
+        if (nt_d)
+            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa_c<72, true, false>), grid, blk, 0, s, v2c,
+                                                     msa_codes(scratch), msa_rec(scratch, c2v_tiles, E), active, M, E,
+                                                     t0, full_lanes, ResStep{}));
+        else
+            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa_c<72, false, false>), grid, blk, 0, s, v2c,
+                                                     msa_codes(scratch), msa_rec(scratch, c2v_tiles, E), active, M, E,
+                                                     t0, full_lanes, ResStep{}));
         return LDPC_OK;
     }
     if (reg72) {
@@ -530,14 +566,20 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         const uint8_t* codes = msa_codes(scratch);
         const double* rec = msa_rec(scratch, c2v_tiles, E);
         LAUNCH_ON(s, K_VAR, {
-            if (cpw == 1) var_msa_c<1>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
-            else if (cpw == 2) var_msa_c<2>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
-            else var_msa_c<4>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
+            if (nt_d) {
+                if (cpw == 1) var_msa_c<true, 1>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
+                else if (cpw == 2) var_msa_c<true, 2>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
+                else var_msa_c<true, 4>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
+            } else {  // resident pool: keep v2c cached
+                if (cpw == 1) var_msa_c<false, 1>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
+                else if (cpw == 2) var_msa_c<false, 2>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
+                else var_msa_c<false, 4>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes);
+            }
         });
         return LDPC_OK;
     }
     // (the resident pool always takes k_var_m: it writes the finished lanes' outputs)
-    if (reg8 && (res || (var_cpw > 1 && nt_d)) && !lr_csc && N % (4 * var_cpw) == 0) {
+    if (reg8 && (res || syn_fused || syn_split || (var_cpw > 1 && nt_d)) && !lr_csc && N % (4 * var_cpw) == 0) {
         const dim3 gm((unsigned)(N / (4 * var_cpw)), gt);
         LAUNCH_ON(s, K_VAR, var_multi(algo, nt_d, var_cpw, s, gm, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf, full_lanes));
         return LDPC_OK;
@@ -759,6 +801,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     ContOut co{d_hard, d_post, d_iters, d_valid, post_t, prior, msa, post_kind == LDPC_POST_RATIO ? 1 : 0};
     const Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0};
     const bool reg_rowT = d_col_idx_T != nullptr;
+    const int hard_vec = ((uintptr_t)d_hard % 8 == 0 && N % 8 == 0) ? 1 : 0;
     if (res) {
         // resident pool: every step is check (+ the syndrome of the previous
         // step and the lane bookkeeping, ResStep) then variable (+ the
@@ -768,7 +811,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         LDPC_HIP(hipMemsetAsync(d_done, 0, (size_t)tiles * sizeof(unsigned int), stream));
         ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, co};
         const Refill rfr{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
-                         d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0};
+                         d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
         // batches of a few pool fills (the DNA batch) poll every step: the
         // host stops at most kLag steps after the pool empties
         const int every = B <= 8 * cap ? 1 : res_poll;
@@ -780,7 +823,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             rs.cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
             if (poll) LDPC_HIP(hipMemsetAsync(rs.cs.occ_count, 0, sizeof(unsigned long long), stream));
             rstep = &rs;
-            rc = launch_check(stream, v2c, 0, (unsigned)tiles);
+            rc = launch_check(stream, c2v, 0, (unsigned)tiles);  // c2v == v2c unless MSA-C
             rstep = nullptr;
             if (rc) break;
             if (poll) {
@@ -788,7 +831,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                                         hipMemcpyDeviceToHost, stream));
                 LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
             }
-            if ((rc = launch_var(stream, v2c, 0, (unsigned)tiles, pt, rfr))) break;
+            if ((rc = launch_var(stream, c2v, 0, (unsigned)tiles, pt, rfr))) break;
             if (poll && pi >= kLag) {
                 const int old = (int)((pi - kLag) % kRing);
                 LDPC_HIP(hipEventSynchronize(ev_ring[old]));
@@ -797,16 +840,62 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         }
         return rc;
     }
+    if (syn_fused) {
+        // grouped steps with the syndrome fused into each group's check
+        // launch (as the resident pool); polled every step, kLag behind
+        LDPC_HIP(hipMemsetAsync(d_unsat, 0, (size_t)tiles * sizeof(unsigned long long), stream));
+        LDPC_HIP(hipMemsetAsync(d_done, 0, (size_t)tiles * sizeof(unsigned int), stream));
+        ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, co};
+        const Refill rfr{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
+                         d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
+        bool low = false;
+        for (int64_t s = 0;; s++) {
+            const int slot = (int)(s % kRing);
+            rs.cs.occ_count = d_ctr + 1 + slot;
+            LDPC_HIP(hipMemsetAsync(rs.cs.occ_count, 0, sizeof(unsigned long long), stream));
+            const int64_t gstep = low ? std::max(group_tiles, c2v_tiles) : group_tiles;
+            for (int64_t t0 = 0; t0 < tiles; t0 += gstep) {
+                const unsigned gt = (unsigned)std::min<int64_t>(gstep, tiles - t0);
+                rstep = &rs;
+                int rc = launch_check(stream, c2v, t0, gt);
+                rstep = nullptr;
+                if (rc) return rc;
+                if ((rc = launch_var(stream, c2v, t0, gt, pt, rfr))) return rc;
+            }
+            LDPC_HIP(hipMemcpyAsync(h_occ + slot, rs.cs.occ_count, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                    stream));
+            LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
+            if (s >= kLag) {
+                const int old = (int)((s - kLag) % kRing);
+                LDPC_HIP(hipEventSynchronize(ev_ring[old]));
+                if (h_occ[old] == 0) break;
+                low = h_occ[old] * 32 < (unsigned long long)(tiles * 64);
+            }
+        }
+        return LDPC_OK;
+    }
     // While the pool is mostly occupied, launch per tile group (c2v stays in the
     // Infinity Cache); once the input is drained and few lanes remain, one
     // check + one variable launch over all tiles per step (the tail is launch-
     // bound, and the c2v traffic is small).  `low` lags the device by kLag.
     bool low = false;
+    ResStep rss{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, co};
+    const Refill rfs{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
+                     d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
+    const bool split = syn_split > 0 && reg_rowT && g->dc_max == 72;
+    if (split) {
+        LDPC_HIP(hipMemsetAsync(d_unsat, 0, (size_t)tiles * sizeof(unsigned long long), stream));
+        LDPC_HIP(hipMemsetAsync(d_done, 0, (size_t)tiles * sizeof(unsigned int), stream));
+    }
     for (int64_t s = 0;; s++) {
         const int slot = (int)(s % kRing);
         cs.occ_count = d_ctr + 1 + slot;
+        rss.cs.occ_count = cs.occ_count;
         LDPC_HIP(hipMemsetAsync(cs.occ_count, 0, sizeof(unsigned long long), stream));
-        if (reg_rowT)
+        if (split)
+            LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome_split<72>, dim3((unsigned)syn_split, (unsigned)tiles), dim3(256),
+                                             0, stream, M, rss));
+        else if (reg_rowT)
             LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome_cont<72>, dim3((unsigned)tiles), dim3(1024), 0, stream, hard,
                                              d_row_ptr, d_col_idx, d_col_idx_T, M, N, max_iter, cs, co));
         else
@@ -819,7 +908,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             const unsigned gt = (unsigned)std::min<int64_t>(gstep, tiles - t0);
             int rc;
             if ((rc = launch_check(stream, c2v, t0, gt))) return rc;
-            if ((rc = launch_var(stream, c2v, t0, gt, pt, rf))) return rc;
+            if ((rc = launch_var(stream, c2v, t0, gt, pt, split ? rfs : rf))) return rc;
         }
         if (s >= kLag) {
             const int old = (int)((s - kLag) % kRing);

@@ -23,6 +23,7 @@ struct Refill {
     uint8_t* hard_out;      // [B][N]
     double* post_out;       // [B][N] or nullptr
     int post_ratio;
+    int hard_vec;           // hard_out is 8-byte aligned and N % 8 == 0: packed per-lane stores
 };
 
 struct ContState {

@@ -65,6 +65,28 @@ __device__ __forceinline__ void st(double* p, double v)
     else *p = v;
 }
 
+// The finished codeword's hard bits of the wave's CPW consecutive columns
+// (pre-update ballots), one CPW-byte store per lane when the output is
+// aligned for it (Refill::hard_vec), else byte stores.
+template <int CPW>
+__device__ __forceinline__ void store_fin_hard(const Refill& rf, const uint64_t* __restrict__ hw, int64_t fb,
+                                               int32_t N, int32_t j0, int lane)
+{
+    uint64_t v = 0;
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) v |= ((hw[c] >> lane) & 1ull) << (8 * c);
+    uint8_t* p = rf.hard_out + (size_t)fb * N + j0;
+    if (rf.hard_vec) {
+        if constexpr (CPW == 8) *reinterpret_cast<uint64_t*>(p) = v;
+        else if constexpr (CPW == 4) *reinterpret_cast<uint32_t*>(p) = (uint32_t)v;
+        else if constexpr (CPW == 2) *reinterpret_cast<uint16_t*>(p) = (uint16_t)v;
+        else *p = (uint8_t)v;
+    } else {
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) p[c] = (uint8_t)(v >> (8 * c));
+    }
+}
+
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
 {
     x += 0x9E3779B97F4A7C15ull;
@@ -562,23 +584,23 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
             for (int s = 0; s < DV; ++s) l[c][s] = c2v[(tl + (size_t)eid[c][s]) * TILE + lane];
         }
     }
+    if (CONT && fl) {  // finished codeword: hard bits of its exit (ballots before this step's update)
+        uint64_t hw[CPW];
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) hw[c] = hard[(size_t)t * N + j0 + c];
+        store_fin_hard<CPW>(rf, hw, fb, N, j0, lane);
+    }
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
         const int32_t j = j0 + c;
         const size_t pj = ((size_t)t * N + j) * TILE + lane;
-        if (CONT && fm != 0ull) {  // finished codeword: hard bit (+ posterior) of its exit
-            const uint64_t hw = hard[(size_t)t * N + j];
-            if (fl) {
-                const size_t ob = (size_t)fb * N + j;
-                rf.hard_out[ob] = (uint8_t)((hw >> lane) & 1ull);
-                if (rf.post_out) {
-                    const double pv = fn > 0 ? post[pj] : prior[pj];
-                    if (MSA) rf.post_out[ob] = pv;
-                    else {
-                        const double P = __builtin_isnan(pv) ? 1.0 : pv;
-                        rf.post_out[ob] = rf.post_ratio ? P : log(P);
-                    }
-                }
+        if (CONT && fl && rf.post_out) {  // finished codeword: posterior of its exit
+            const size_t ob = (size_t)fb * N + j;
+            const double pv = fn > 0 ? post[pj] : prior[pj];
+            if (MSA) rf.post_out[ob] = pv;
+            else {
+                const double P = __builtin_isnan(pv) ? 1.0 : pv;
+                rf.post_out[ob] = rf.post_ratio ? P : log(P);
             }
         }
         bool h = false;
@@ -945,17 +967,10 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
 constexpr int MSA_REC_PLANES = 4;
 
 template <int DC, bool NT>
-__global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, uint8_t* __restrict__ codes,
-                                                     double* __restrict__ rec, const uint64_t* __restrict__ active,
-                                                     int32_t M, int64_t E, int64_t t0, int full_lanes)
+__device__ __forceinline__ void check_msa_c_row(const double* __restrict__ v2c, uint8_t* __restrict__ codes,
+                                                double* __restrict__ rec, int32_t M, int64_t E, int64_t t, int32_t row)
 {
-    static_assert(DC >= 2 && DC <= 96, "row degree");
     const int lane = lane_id();
-    const int32_t row = blockIdx.x * 4 + wave_id();
-    const int64_t t = t0 + blockIdx.y;
-    if (row >= M) return;
-    const uint64_t act = active[t];
-    if ((full_lanes & 1) ? act == 0 : !((act >> lane) & 1ull)) return;
     const double* __restrict__ src = v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
     double x[DC];
 #pragma unroll
@@ -993,6 +1008,37 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     }
 }
 
+// SYN (resident pool, ResStep): as k_check_bp's -- the lanes run are the
+// tile's occupied ones, each wave also takes its row's parity over the
+// previous variable phase's ballots, every block ends in res_arrive.
+template <int DC, bool NT, bool SYN>
+__global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, uint8_t* __restrict__ codes,
+                                                     double* __restrict__ rec, const uint64_t* __restrict__ active,
+                                                     int32_t M, int64_t E, int64_t t0, int full_lanes, ResStep rs)
+{
+    static_assert(DC >= 2 && DC <= 96, "row degree");
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = t0 + blockIdx.y;
+    const uint64_t act = SYN ? rs.cs.occupied[t] : active[t];
+    const bool run = row < M && ((full_lanes & 1) ? act != 0 : ((act >> lane) & 1ull));
+    if constexpr (!SYN) {
+        if (!run) return;
+    }
+    uint64_t par = 0;
+    int32_t ln0 = 0;
+    int64_t b0 = 0;
+    if (SYN && act != 0) {
+        if (threadIdx.x < TILE && ((act >> lane) & 1ull)) {
+            ln0 = rs.cs.lane_n[t * TILE + lane];
+            b0 = rs.cs.lane_b[t * TILE + lane];
+        }
+        if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
+    }
+    if (run) check_msa_c_row<DC, NT>(v2c, codes, rec, M, E, t, row);
+    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0);
+}
+
 // Min-sum variable phase on compressed messages (arithmetic of k_var_m<MSA>).
 // 1-D grid of gt * (N / (4 CPW)) blocks; block L works on group tile L % gt.
 // Workgroups are dispatched to the 8 XCDs round-robin, so when gt divides 8
@@ -1015,9 +1061,19 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
     const uint64_t act = active[t];
     const uint64_t frm = CONT ? rf.fresh[t] : 0ull;
     const uint64_t touched = act | frm;
-    if (touched == 0) return;
+    // resident pool: lanes whose codeword finished at this step's syndrome
+    // (outputs written here, before a refill overwrites the lane; as k_var_m)
+    const uint64_t fm = (CONT && rf.fin) ? rf.fin[t] : 0ull;
+    if (touched == 0 && fm == 0) return;
     const bool live = (act >> lane) & 1ull;
     const bool fr = CONT && ((frm >> lane) & 1ull);
+    const bool fl = (fm >> lane) & 1ull;
+    int64_t fb = 0;
+    int32_t fn = 0;
+    if (fl) {
+        fb = rf.fin_b[t * TILE + lane];
+        fn = rf.fin_n[t * TILE + lane];
+    }
     const size_t tb = (size_t)t * E;
     int32_t eid[CPW][DV], rid[CPW][DV];
 #pragma unroll
@@ -1093,10 +1149,20 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
                 l[c][s] = (double)sign * l[c][s];
             }
     }
+    if (CONT && fl) {  // finished codeword: hard bits of its exit (ballots before this step's update)
+        uint64_t hw[CPW];
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) hw[c] = hard[(size_t)t * N + j0 + c];
+        store_fin_hard<CPW>(rf, hw, fb, N, j0, lane);
+    }
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
         const int32_t j = j0 + c;
         const size_t pj = ((size_t)t * N + j) * TILE + lane;
+        if (CONT && fl && rf.post_out) {  // finished codeword: posterior L of its exit
+            const size_t ob = (size_t)fb * N + j;
+            rf.post_out[ob] = fn > 0 ? post[pj] : prior[pj];
+        }
         bool h = false;
         double dv[DV];
 #pragma unroll
@@ -1225,6 +1291,54 @@ __global__ __launch_bounds__(1024) void k_syndrome_cont(const uint64_t* __restri
     }
     __syncthreads();
     if (s_fin) cont_outputs(t, s_fin, h, N, co, s_b, s_n);
+}
+
+// Continuous-batching syndrome spread over gridDim.x blocks per tile (the
+// k_syndrome_cont step with the resident pool's last-block bookkeeping,
+// res_arrive): 16 tiles' syndromes in one block per tile left 240 of the 256
+// CUs idle for ~64 us per step.  A wave takes 8 rows, lane (part, row) XORs
+// the ballots of edges part*KP .. part*KP+KP-1 of its row (KP = ceil(DC/8)),
+// the parts are XOR-combined across lanes, and the rows OR-combined; the
+// tile's last block runs cont_lanes and hands the finished lanes to the
+// variable kernel (Refill::fin), which writes their outputs.
+template <int DC>
+__global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs)
+{
+    constexpr int KP = (DC + 7) / 8;
+    const int64_t t = blockIdx.y;
+    const uint64_t occ = rs.cs.occupied[t];
+    const int lane = lane_id();
+    int32_t ln0 = 0;
+    int64_t b0 = 0;
+    uint64_t u = 0;
+    if (occ) {
+        if (threadIdx.x < TILE && ((occ >> lane) & 1ull)) {
+            ln0 = rs.cs.lane_n[t * TILE + lane];
+            b0 = rs.cs.lane_b[t * TILE + lane];
+        }
+        const uint64_t* __restrict__ h = rs.hard + (size_t)t * rs.N;
+        const int part = lane >> 3;
+        for (int32_t r0 = (int32_t)(blockIdx.x * 4 + wave_id()) * 8; r0 < M; r0 += (int32_t)gridDim.x * 32) {
+            const int32_t row = r0 + (lane & 7);
+            uint64_t p = 0;
+            if (row < M) {
+                const int32_t* __restrict__ cols = rs.col_idx + (size_t)row * DC;
+#pragma unroll
+                for (int q = 0; q < KP; ++q) {
+                    const int k = part * KP + q;
+                    if (k < DC) p ^= h[cols[k]];
+                }
+            }
+            p ^= shfl_xor_u64(p, 8);
+            p ^= shfl_xor_u64(p, 16);
+            p ^= shfl_xor_u64(p, 32);
+            u |= p;
+        }
+        u |= shfl_xor_u64(u, 1);
+        u |= shfl_xor_u64(u, 2);
+        u |= shfl_xor_u64(u, 4);
+    }
+    res_arrive(t, occ, u, rs, ln0, b0);
 }
 
 // hard ballots -> [b][N] u8 (the reference's dblk / dec_*.txt bits)

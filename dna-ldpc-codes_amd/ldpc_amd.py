@@ -429,6 +429,8 @@ class Engine:
         self.continuous = bool(fl.value & 8)
         self.msa_compressed = bool(fl.value & 16)  # min-sum c2v as per-row records + per-edge codes
         self.resident = bool(fl.value & 32)  # in-place pool of a few tiles (LDPC_RES)
+        self.syndrome_split = bool(fl.value & 64)  # multi-block continuous-mode syndrome (LDPC_SYN_SPLIT)
+        self.syndrome_fused = bool(fl.value & 128)  # syndrome in the grouped check launches (LDPC_SYN_FUSED)
 
     def decode(self, d_in, in_kind: int, B: int, max_iter: int, d_hard=None, d_post=None, post_kind=POST_LLR,
                d_iters=None, d_valid=None):

@@ -213,7 +213,10 @@ int ldpc_engine_set_params(ldpc_engine *e, int32_t msa_precision, double msa_ste
 /* The schedule an engine runs with: resident codewords per pass (the lane
  * pool in continuous mode), group tiles, and flags with the bits of
  * ldpc_engine_create_ex plus bit 4 = compressed min-sum check->variable
- * messages (env LDPC_MSA_C); bit 5 as in create_ex. */
+ * messages (env LDPC_MSA_C); bit 5 as in create_ex; bit 6 =
+ * continuous-mode syndrome spread over several blocks per tile (env
+ * LDPC_SYN_SPLIT); bit 7 = syndrome fused into the grouped check launches
+ * (env LDPC_SYN_FUSED). */
 int ldpc_engine_info(ldpc_engine *e, int64_t *cap, int64_t *group_tiles, int32_t *flags);
 int ldpc_engine_stats(ldpc_engine *e, ldpc_kernel_stats *out);
 

@@ -233,6 +233,20 @@ def test_engine_device_resident_matches_host_api(gpu, G, og, codewords):
     llr = synth.bsc_llrs(codewords, 0, B, seed=77, p=0.005)
     rh, _, rit, rv = og.decode_batch(llr, 50, threads=8, want_post=False)
     assert np.array_equal(it, rit) and np.array_equal(v, rv) and np.array_equal(h, rh)
+    # hard output at an odd device address: the finished-lane hard-bit stores
+    # of the variable kernels fall back from packed to byte stores
+    for algo, kind in (("bp", L.IN_LR), ("msa", L.IN_LLR)):
+        e2 = L.Engine(G, 0, algo)
+        if algo == "msa":
+            e2.gen_bsc(din.at(0), L.IN_LLR, 0, B, cwbuf.at(0), 272, 77, 0.002, synth.LLR_UNIT)
+        dh2 = L.DeviceBuffer(0, B * N + 8)
+        e2.decode(din.at(0), kind, B, 50, dh2.at(3), None, L.POST_LLR, dit.at(0), dv.at(0))
+        e2.sync()
+        h2 = dh2.download(np.empty(B * N + 8, np.uint8))[3:3 + B * N].reshape(B, N)
+        it2 = dit.download(np.empty(B, np.int32))
+        llr2 = synth.bsc_llrs(codewords, 0, B, seed=77, p=0.005 if algo == "bp" else 0.002)
+        rh2, _, rit2, _ = og.decode_batch(llr2, 50, algo=0 if algo == "bp" else 1, threads=8, want_post=False)
+        assert np.array_equal(it2, rit2) and np.array_equal(h2, rh2)
 
 
 def test_device_exp_matches_host_on_dna_alphabet(gpu, G, codewords):
@@ -371,3 +385,97 @@ def test_min_sum_compressed_messages_bitexact(gpu, og, codewords, monkeypatch, m
     nan = np.isnan(ref_p)
     assert np.array_equal(np.isnan(p), nan)
     assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64))
+
+
+@pytest.mark.parametrize("tiles,poll,cpw", [(2, 4, 4), (1, 1, 2), (3, 2, 4), (4, 7, 1)])
+def test_min_sum_compressed_resident_pool_bitexact(gpu, og, codewords, monkeypatch, tiles, poll, cpw):
+    """Resident pool for compressed min-sum (LDPC_RES_MSA_C): k_check_msa_c
+    with the fused syndrome + last-block lane bookkeeping (SYN), k_var_msa_c
+    writing the finished lanes' hard bits / posterior before refilling them.
+    Bit-exact across pool sizes (1-4 tiles, the XCD-affine order with and
+    without gt | 8), poll intervals, mixed exits, non-converging lanes,
+    max_iter 0, batches smaller than the pool and NaN / inf / -0.0 inputs."""
+    monkeypatch.setenv("LDPC_MSA_C", "1")
+    monkeypatch.setenv("LDPC_RES_MSA_C", "1")
+    monkeypatch.setenv("LDPC_RES_TILES_MSA_C", str(tiles))
+    monkeypatch.setenv("LDPC_RES_POLL", str(poll))
+    monkeypatch.setenv("LDPC_VAR_CPW", str(cpw))
+    monkeypatch.setenv("LDPC_CONT", "1")
+    G2 = gpu.Graph(PCHK)
+    llr = synth.bsc_llrs(codewords, 0, 300, seed=2026, p=0.002)
+    _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa")
+    assert len(np.unique(it)) > 2
+    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 70, seed=5, p=0.01), 12, algo="msa")
+    _cmp(G2, og, llr[:70], 0, algo="msa")
+    _cmp(G2, og, llr[:5], 50, algo="msa")
+    rng = np.random.default_rng(17)
+    llr = synth.bsc_llrs(codewords, 0, 130, seed=11, p=0.004)
+    llr[rng.random(llr.shape) < 0.003] = np.nan
+    llr[rng.random(llr.shape) < 0.002] = np.inf
+    llr[rng.random(llr.shape) < 0.002] = -np.inf
+    llr[rng.random(llr.shape) < 0.01] = -0.0
+    llr[:2] = np.nan
+    ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 20, algo=1, post_mode=0, threads=8)
+    h, p, it, v = G2.decode(llr, max_iter=20, algo="msa", post="llr")
+    assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
+    nan = np.isnan(ref_p)
+    assert np.array_equal(np.isnan(p), nan)
+    assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64))
+
+
+@pytest.mark.parametrize("algo,msa_c,group,chunk", [("bp", 0, 3, 256), ("bp", 0, 1, 128), ("msa", 1, 4, 512),
+                                                    ("msa", 1, 2, 128), ("msa", 0, 3, 192)])
+def test_fused_syndrome_grouped_bitexact(gpu, og, codewords, monkeypatch, algo, msa_c, group, chunk):
+    """LDPC_SYN_FUSED (engine.hip run_cont `syn_fused`): the grouped
+    continuous schedule with each group's check launch computing the
+    syndrome of its tiles and the lane bookkeeping (ResStep), and the
+    variable launch writing finished codewords' outputs before the refill.
+    Pools smaller than the batch (many refills), groups that do not divide
+    the pool, mixed exits, max_iter 0, posterior at each codeword's exit."""
+    monkeypatch.setenv("LDPC_SYN_FUSED", "1")
+    monkeypatch.setenv("LDPC_CONT", "1")
+    monkeypatch.setenv("LDPC_RES", "0")
+    monkeypatch.setenv("LDPC_RES_MSA_C", "0")
+    monkeypatch.setenv("LDPC_MSA_C", str(msa_c))
+    monkeypatch.setenv("LDPC_GROUP_TILES", str(group))
+    G2 = gpu.Graph(PCHK)
+    if algo == "bp":
+        llr = np.concatenate([synth.bsc_llrs(codewords, 0, 300, seed=3, p=0.003),
+                              synth.bsc_llrs(codewords, 300, 100, seed=2026, p=0.02)])
+        _, _, it, _ = _cmp(G2, og, llr, 30, chunk=chunk)
+        llr = synth.dna_like_llrs(codewords, seed=1, reads=57000)[:150]
+        _cmp(G2, og, llr, 60, chunk=chunk)
+    else:
+        llr = synth.bsc_llrs(codewords, 0, 400, seed=2026, p=0.002)
+        _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", chunk=chunk)
+    assert len(np.unique(it)) > 2
+    _cmp(G2, og, llr[:70], 0, algo=algo, chunk=chunk)
+    _cmp(G2, og, llr[:3], 20, algo=algo, chunk=chunk)
+
+
+@pytest.mark.parametrize("algo,msa_c,group,chunk,split", [("msa", 1, 4, 1024, 16), ("msa", 1, 2, 128, 3),
+                                                          ("msa", 0, 3, 192, 64), ("bp", 0, 3, 256, 8),
+                                                          ("bp", 0, 1, 128, 1)])
+def test_split_syndrome_bitexact(gpu, og, codewords, monkeypatch, algo, msa_c, group, chunk, split):
+    """LDPC_SYN_SPLIT (kernels.hpp k_syndrome_split): the continuous-mode
+    syndrome spread over `split` blocks per tile (8 rows per wave, 8 edge
+    parts per row), the last block per tile running the lane bookkeeping and
+    the variable launch writing the finished codewords' outputs."""
+    monkeypatch.setenv("LDPC_SYN_SPLIT", str(split))
+    monkeypatch.setenv("LDPC_SYN_FUSED", "0")
+    monkeypatch.setenv("LDPC_CONT", "1")
+    monkeypatch.setenv("LDPC_RES", "0")
+    monkeypatch.setenv("LDPC_RES_MSA_C", "0")
+    monkeypatch.setenv("LDPC_MSA_C", str(msa_c))
+    monkeypatch.setenv("LDPC_GROUP_TILES", str(group))
+    G2 = gpu.Graph(PCHK)
+    if algo == "bp":
+        llr = np.concatenate([synth.bsc_llrs(codewords, 0, 300, seed=3, p=0.003),
+                              synth.bsc_llrs(codewords, 300, 100, seed=2026, p=0.02)])
+        _, _, it, _ = _cmp(G2, og, llr, 30, chunk=chunk)
+    else:
+        llr = synth.bsc_llrs(codewords, 0, 400, seed=2026, p=0.002)
+        _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", chunk=chunk)
+    assert len(np.unique(it)) > 2
+    _cmp(G2, og, llr[:70], 0, algo=algo, chunk=chunk)
+    _cmp(G2, og, llr[:3], 20, algo=algo, chunk=chunk)

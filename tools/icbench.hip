@@ -183,7 +183,7 @@ int main(int argc, char** argv)
                 const unsigned nb = (unsigned)(N / (4 * cpw)) * G;
                 float ms = timeit([&] {
                     for (int t0 = 0; t0 + G <= P; t0 += G) {
-                        hipLaunchKernelGGL((k_check_msa_c<72, true>), dim3(M / 4, G), blk, 0, 0, d, codes, rec, active, M, E, (int64_t)t0, 1);
+                        hipLaunchKernelGGL((k_check_msa_c<72, true, false>), dim3(M / 4, G), blk, 0, 0, d, codes, rec, active, M, E, (int64_t)t0, 1, ResStep{});
                         if (cpw == 2) hipLaunchKernelGGL((k_var_msa_c<8, true, false, 2, true>), dim3(nb), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)t0, (uint32_t)G, rf, 1);
                         else hipLaunchKernelGGL((k_var_msa_c<8, true, false, 4, true>), dim3(nb), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)t0, (uint32_t)G, rf, 1);
                     }
@@ -198,7 +198,7 @@ int main(int argc, char** argv)
                 const unsigned nb = (unsigned)(N / (4 * cpw)) * G;
                 float ms = timeit([&] {
                     for (int t0 = 0; t0 + G <= P; t0 += G) {
-                        hipLaunchKernelGGL((k_check_msa_c<72, true>), dim3(M / 4, G), blk, 0, 0, d, codes, rec, active, M, E, (int64_t)t0, 1);
+                        hipLaunchKernelGGL((k_check_msa_c<72, true, false>), dim3(M / 4, G), blk, 0, 0, d, codes, rec, active, M, E, (int64_t)t0, 1, ResStep{});
                         if (cpw == 1) hipLaunchKernelGGL((k_var_msa_c<8, true, false, 1>), dim3(nb), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)t0, (uint32_t)G, rf, 1);
                         else if (cpw == 2) hipLaunchKernelGGL((k_var_msa_c<8, true, false, 2>), dim3(nb), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)t0, (uint32_t)G, rf, 1);
                         else hipLaunchKernelGGL((k_var_msa_c<8, true, false, 4>), dim3(nb), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)t0, (uint32_t)G, rf, 1);
@@ -218,7 +218,7 @@ int main(int argc, char** argv)
             float mc = 0, mv = 0;
             for (int it = 0; it < 12; it++) {
                 CK(hipEventRecord(a));
-                hipLaunchKernelGGL((k_check_msa_c<72, true>), dim3(M / 4, 8), blk, 0, 0, d, codes, rec, active, M, E, (int64_t)0, 1);
+                hipLaunchKernelGGL((k_check_msa_c<72, true, false>), dim3(M / 4, 8), blk, 0, 0, d, codes, rec, active, M, E, (int64_t)0, 1, ResStep{});
                 CK(hipEventRecord(b));
                 hipLaunchKernelGGL((k_var_msa_c<8, true, false, 2>), dim3((unsigned)(N / 8) * 8), blk, 0, 0, codes, rec, d, prior, hard, active, d_col_edge, d_col_row, (double*)nullptr, N, M, E, (int64_t)0, 8u, rf, 1);
                 CK(hipEventRecord(c));
