@@ -45,6 +45,7 @@ constexpr int64_t kDefaultVarCpw = 4;  // LDPC_VAR_CPW (A/B over two boxes: +2.6
 constexpr int64_t kDefaultRes = 1;       // LDPC_RES: resident in-place pool for BP / fp64 min-sum in continuous mode
 constexpr int64_t kDefaultResTiles = 3;  // LDPC_RES_TILES: pool tiles (3 x 85 MB ~ the 256 MB Infinity Cache; A/B)
 constexpr int64_t kDefaultResPoll = 8;
+constexpr int64_t kResAutoMaxTiles = 4;      // explicit pools above this many tiles: grouped schedule unless LDPC_RES is set
 constexpr int64_t kDefaultSynSplit = 32;     // LDPC_SYN_SPLIT: syndrome blocks per tile in continuous mode (0: one block, k_syndrome_cont; A/B min-sum config 5 +5-6 %)
 constexpr int64_t kDefaultSynFused = 0;      // LDPC_SYN_FUSED: grouped continuous mode, syndrome fused into the check kernel
 constexpr int64_t kDefaultResMsaC = 0;       // LDPC_RES_MSA_C: resident pool for compressed min-sum
@@ -125,9 +126,17 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     // messages they are computed from (each row's / column's edges are read
     // into registers before its outputs are stored), no c2v scratch
     // (compressed min-sum: its own switch, LDPC_RES_MSA_C; k_var_msa_c needs N % 16)
-    if (res_mode < 0)
+    bool res_auto = false;  // neither the caller nor the environment chose
+    if (res_mode < 0) {
+        const char* ev = std::getenv(msa_c ? "LDPC_RES_MSA_C" : "LDPC_RES");
+        res_auto = !(ev && *ev);
         res_mode = (int)(msa_c ? env_int("LDPC_RES_MSA_C", kDefaultResMsaC) : env_int("LDPC_RES", kDefaultRes));
+    }
     res = res_mode != 0 && cont && (msa_c ? g->N % 16 == 0 : g->N % 32 == 0);  // k_var_m at any columns-per-wave
+    // by default the resident pool is the Infinity-Cache-sized one: a caller's
+    // explicit larger pool (the host API's chunks, the DNA batch) runs the
+    // grouped schedule (A/B, 272-codeword DNA batch at cap 320: 193k -> 250k cw/s)
+    if (res && res_auto && chunk > kResAutoMaxTiles * 64) res = false;
     if (res) {
         nt = 0;  // the pool is meant to stay cached
         pipelined = 0;
