@@ -45,7 +45,8 @@ constexpr int64_t kDefaultVarCpw = 4;  // LDPC_VAR_CPW (A/B over two boxes: +2.6
 constexpr int64_t kDefaultRes = 1;       // LDPC_RES: resident in-place pool for BP / fp64 min-sum in continuous mode
 constexpr int64_t kDefaultResTiles = 3;  // LDPC_RES_TILES: pool tiles (3 x 85 MB ~ the 256 MB Infinity Cache; A/B)
 constexpr int64_t kDefaultResPoll = 8;
-constexpr int64_t kResAutoMaxTiles = 4;      // explicit pools above this many tiles: grouped schedule unless LDPC_RES is set
+constexpr int64_t kResAutoMaxTiles = 4;
+constexpr int64_t kDefaultResSyn = 0;        // LDPC_RES_SYN: resident pool syndrome, 0 = fused into the check kernel, >0 = k_syndrome_split blocks per tile      // explicit pools above this many tiles: grouped schedule unless LDPC_RES is set
 constexpr int64_t kDefaultSynSplit = 32;     // LDPC_SYN_SPLIT: syndrome blocks per tile in continuous mode (0: one block, k_syndrome_cont; A/B min-sum config 5 +5-6 %)
 constexpr int64_t kDefaultSynFused = 0;      // LDPC_SYN_FUSED: grouped continuous mode, syndrome fused into the check kernel
 constexpr int64_t kDefaultResMsaC = 0;       // LDPC_RES_MSA_C: resident pool for compressed min-sum
@@ -142,6 +143,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         pipelined = 0;
         csc = 0;
         res_poll = (int)std::max<int64_t>(1, env_int("LDPC_RES_POLL", kDefaultResPoll));
+        res_syn_split = (int)std::max<int64_t>(0, std::min<int64_t>(env_int("LDPC_RES_SYN", kDefaultResSyn), 256));
     }
     if (chunk <= 0) {
         size_t fr = 0, tot = 0;
@@ -831,9 +833,15 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             const int slot = (int)(pi % kRing);
             rs.cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
             if (poll) LDPC_HIP(hipMemsetAsync(rs.cs.occ_count, 0, sizeof(unsigned long long), stream));
-            rstep = &rs;
-            rc = launch_check(stream, c2v, 0, (unsigned)tiles);  // c2v == v2c unless MSA-C
-            rstep = nullptr;
+            if (res_syn_split > 0) {  // separate multi-block syndrome, then a plain in-place check
+                LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome_split<72>, dim3((unsigned)res_syn_split, (unsigned)tiles),
+                                                 dim3(256), 0, stream, M, rs));
+                rc = launch_check(stream, c2v, 0, (unsigned)tiles);
+            } else {
+                rstep = &rs;
+                rc = launch_check(stream, c2v, 0, (unsigned)tiles);  // c2v == v2c unless MSA-C
+                rstep = nullptr;
+            }
             if (rc) break;
             if (poll) {
                 LDPC_HIP(hipMemcpyAsync(h_occ + slot, rs.cs.occ_count, sizeof(unsigned long long),

@@ -479,3 +479,27 @@ def test_split_syndrome_bitexact(gpu, og, codewords, monkeypatch, algo, msa_c, g
     assert len(np.unique(it)) > 2
     _cmp(G2, og, llr[:70], 0, algo=algo, chunk=chunk)
     _cmp(G2, og, llr[:3], 20, algo=algo, chunk=chunk)
+
+
+@pytest.mark.parametrize("algo,msa_c,tiles,split", [("bp", 0, 3, 32), ("bp", 0, 1, 5), ("msa", 0, 2, 64), ("msa", 1, 2, 16)])
+def test_resident_pool_split_syndrome_bitexact(gpu, og, codewords, monkeypatch, algo, msa_c, tiles, split):
+    """LDPC_RES_SYN > 0: the resident pool with a separate multi-block
+    syndrome launch (k_syndrome_split) before a plain in-place check."""
+    monkeypatch.setenv("LDPC_RES", "1")
+    monkeypatch.setenv("LDPC_RES_MSA_C", "1")
+    monkeypatch.setenv("LDPC_RES_SYN", str(split))
+    monkeypatch.setenv("LDPC_RES_TILES", str(tiles))
+    monkeypatch.setenv("LDPC_RES_TILES_MSA_C", str(tiles))
+    monkeypatch.setenv("LDPC_MSA_C", str(msa_c))
+    monkeypatch.setenv("LDPC_CONT", "1")
+    G2 = gpu.Graph(PCHK)
+    if algo == "bp":
+        llr = np.concatenate([synth.bsc_llrs(codewords, 0, 200, seed=3, p=0.003),
+                              synth.bsc_llrs(codewords, 200, 100, seed=2026, p=0.02)])
+        _, _, it, _ = _cmp(G2, og, llr, 30)
+    else:
+        llr = synth.bsc_llrs(codewords, 0, 300, seed=2026, p=0.002)
+        _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa")
+    assert len(np.unique(it)) > 2
+    _cmp(G2, og, llr[:70], 0, algo=algo)
+    _cmp(G2, og, llr[:3], 20, algo=algo)
