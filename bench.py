@@ -125,6 +125,7 @@ def bench_dna272(args):
         og.decode_batch(llr, max_iter, threads=threads, want_post=False)
         el_c = time.perf_counter() - t
         out["cpu_baseline"] = {"value": round(B / el_c, 2), "unit": "codewords/s", "cores": threads, "kind": "port",
+                               "per_core": round(B / el_c / threads, 2),
                                "sample": f"the same 272 codewords, {max_iter} max iters, oracle on {threads} threads"}
     print(json.dumps(out), flush=True)
 
@@ -154,6 +155,7 @@ def cpu_baseline(args, llr_fn, N):
     og.decode_batch(llr, args.max_iter, algo=algo, threads=threads, want_post=False)
     el = time.perf_counter() - t
     return {"value": round(n / el, 3), "unit": "codewords/s", "cores": threads, "kind": "port",
+            "per_core": round(n / el / threads, 3),
             "sample": f"{n} codewords of the same BSC(p={args.p}) workload (indices {threads}..{threads + n - 1}), "
                       f"{args.max_iter} iters, oracle/ldpc_oracle.c on {threads} host threads, {el:.1f} s"}
 
