@@ -1,0 +1,44 @@
+"""bench.py end to end on a small batch: the one-JSON-line contract the
+driver reads (metric / value / roofline / cpu_baseline), for the default BP
+workload, min-sum, and the DNA batch."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+METRIC = "decoded codewords/sec (n=18432, m=2048, 50 BP iters) at 1/2/4/8 GPUs; % HBM roofline"
+
+
+def _bench(*args):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["metric"] == METRIC and out["unit"] == "codewords/s" and out["n_gpus"] == 1
+    assert out["value"] > 0 and out["higher_is_better"] is True and out["scaling"] == "weak"
+    return out
+
+
+@pytest.mark.parametrize("algo,p", [("bp", 0.02), ("msa", 0.002)])
+def test_bench_bsc_line(gpu, algo, p):
+    out = _bench("--algo", algo, "--p", str(p), "--batch-per-gpu", "2048", "--steps", "1", "--warmup", "1",
+                 "--cpu-seconds", "1")
+    assert out["steps"] == 1 and out["dtype"] == "f64"
+    rl = out["roofline"]
+    assert rl["bound"] == "hbm" and rl["unit"] == "GB/s" and rl["peak"] == 8000.0
+    assert rl["achieved"] > 0 and 0 < rl["frac"] < 1.2
+    cb = out["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["per_core"] > 0
+    if algo == "bp":
+        assert out["config"]["mean_iters"] == 50.0
+
+
+def test_bench_dna272_line(gpu):
+    out = _bench("--workload", "dna272", "--steps", "2", "--warmup", "1")
+    assert out["config"]["genie_ok"] == 272
