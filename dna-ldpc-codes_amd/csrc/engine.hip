@@ -45,8 +45,8 @@ constexpr int64_t kDefaultVarCpw = 4;  // LDPC_VAR_CPW (A/B over two boxes: +2.6
 constexpr int64_t kDefaultRes = 1;       // LDPC_RES: resident in-place pool for BP / fp64 min-sum in continuous mode
 constexpr int64_t kDefaultResTiles = 3;  // LDPC_RES_TILES: pool tiles (3 x 85 MB ~ the 256 MB Infinity Cache; A/B)
 constexpr int64_t kDefaultResPoll = 8;
-constexpr int64_t kResAutoMaxTiles = 4;
-constexpr int64_t kDefaultResSyn = 0;        // LDPC_RES_SYN: resident pool syndrome, 0 = fused into the check kernel, >0 = k_syndrome_split blocks per tile, -1 = accumulated by the variable kernel (BP)      // explicit pools above this many tiles: grouped schedule unless LDPC_RES is set
+constexpr int64_t kResAutoMaxTiles = 4;      // explicit pools above this many tiles: grouped schedule unless LDPC_RES is set
+constexpr int64_t kDefaultResSyn = 0;        // LDPC_RES_SYN: resident pool syndrome, 0 = fused into the check kernel, >0 = k_syndrome_split blocks per tile
 constexpr int64_t kDefaultSynSplit = 32;     // LDPC_SYN_SPLIT: syndrome blocks per tile in continuous mode (0: one block, k_syndrome_cont; A/B min-sum config 5 +5-6 %)
 constexpr int64_t kDefaultSynFused = 0;      // LDPC_SYN_FUSED: grouped continuous mode, syndrome fused into the check kernel
 constexpr int64_t kDefaultResMsaC = 0;       // LDPC_RES_MSA_C: resident pool for compressed min-sum
@@ -81,7 +81,6 @@ Engine::~Engine()
     for (int i = 0; i < kRing; i++)
         if (ev_ring[i]) hipEventDestroy(ev_ring[i]);
     hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge); hipFree(d_col_row);
-    hipFree(d_synacc);
     hipFree(d_unsat); hipFree(d_done); hipFree(d_fin); hipFree(d_fin_b); hipFree(d_fin_n);
     hipFree(v2c); if (c2v != v2c) hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
     hipFree(post_t);
@@ -144,7 +143,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         pipelined = 0;
         csc = 0;
         res_poll = (int)std::max<int64_t>(1, env_int("LDPC_RES_POLL", kDefaultResPoll));
-        res_syn_split = (int)std::max<int64_t>(-1, std::min<int64_t>(env_int("LDPC_RES_SYN", kDefaultResSyn), 256));
+        res_syn_split = (int)std::max<int64_t>(0, std::min<int64_t>(env_int("LDPC_RES_SYN", kDefaultResSyn), 256));
     }
     if (chunk <= 0) {
         size_t fr = 0, tot = 0;
@@ -230,8 +229,6 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         LDPC_HIP(hipMalloc((void**)&d_fin_b, (size_t)cap * sizeof(int64_t)));
         LDPC_HIP(hipMalloc((void**)&d_fin_n, (size_t)cap * sizeof(int32_t)));
     }
-    if (res && res_syn_split < 0 && algo == LDPC_ALGO_BP && g->regular_dc && g->dc_max == 72)
-        LDPC_HIP(hipMalloc((void**)&d_synacc, 2 * (size_t)cap_tiles * g->M * sizeof(unsigned long long)));
     if (res) {
         c2v_tiles = cap_tiles;
         if (msa_c)  // codes + records of the whole pool (13.6 MB per tile for the DNA code)
@@ -827,18 +824,8 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         LDPC_HIP(hipMemsetAsync(d_unsat, 0, (size_t)tiles * sizeof(unsigned long long), stream));
         LDPC_HIP(hipMemsetAsync(d_done, 0, (size_t)tiles * sizeof(unsigned int), stream));
         ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, co};
-        Refill rfr{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
-                   d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
-        // accumulated syndrome (BP, LDPC_RES_SYN < 0): the variable kernel of
-        // step s XORs each stored ballot word into plane s & 1, the check
-        // kernel of step s + 1 takes (and zeroes) its row's word
-        const bool acc = d_synacc != nullptr;
-        const size_t plane = (size_t)cap_tiles * M;
-        if (acc) {
-            LDPC_HIP(hipMemsetAsync(d_synacc, 0, 2 * plane * sizeof(unsigned long long), stream));
-            rfr.syn_dc = g->dc_max;
-            rfr.syn_m = M;
-        }
+        const Refill rfr{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
+                         d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
         // batches of a few pool fills (the DNA batch) poll every step: the
         // host stops at most kLag steps after the pool empties
         const int every = B <= 8 * cap ? 1 : res_poll;
@@ -849,10 +836,6 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             const int slot = (int)(pi % kRing);
             rs.cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
             if (poll) LDPC_HIP(hipMemsetAsync(rs.cs.occ_count, 0, sizeof(unsigned long long), stream));
-            if (acc) {
-                rs.syn_acc = d_synacc + (size_t)((s + 1) & 1) * plane;  // step s - 1's plane
-                rfr.syn_acc = d_synacc + (size_t)(s & 1) * plane;
-            }
             if (res_syn_split > 0) {  // separate multi-block syndrome, then a plain in-place check
                 LAUNCH(K_SYN, hipLaunchKernelGGL(k_syndrome_split<72>, dim3((unsigned)res_syn_split, (unsigned)tiles),
                                                  dim3(256), 0, stream, M, rs));

@@ -47,8 +47,7 @@ struct Engine {
     bool msa_c = false;       // min-sum with compressed c2v (records + codes, k_check_msa_c / k_var_msa_c)
     bool res = false;         // resident pool: a few tiles iterated in place (c2v overwrites v2c), syndrome in the check kernel
     int res_poll = 4;         // res: steps between occupancy polls
-    int res_syn_split = 0;    // res: 0 = syndrome fused into the check kernel, >0 = k_syndrome_split blocks per tile, -1 = accumulated
-    unsigned long long* d_synacc = nullptr;  // res, accumulated syndrome: [2][tile][M] row parity words
+    int res_syn_split = 0;    // res: 0 = syndrome fused into the check kernel, >0 = k_syndrome_split blocks per tile
     int syn_split = 0;        // continuous mode: syndrome blocks per tile (k_syndrome_split; 0: k_syndrome_cont)
     bool syn_fused = false;   // grouped continuous mode: syndrome + lane bookkeeping in the check kernel (ResStep)
     unsigned long long* d_unsat = nullptr;  // res: [tile] syndrome words of the step

@@ -24,10 +24,6 @@ struct Refill {
     double* post_out;       // [B][N] or nullptr
     int post_ratio;
     int hard_vec;           // hard_out is 8-byte aligned and N % 8 == 0: packed per-lane stores
-    // resident pool, accumulated syndrome (LDPC_RES_SYN < 0): every column's
-    // stored ballot word is XORed into the words of its rows ([tile][M])
-    unsigned long long* syn_acc;
-    int32_t syn_dc, syn_m;  // regular row degree (row of edge e = e / dc), rows
 };
 
 struct ContState {
@@ -65,7 +61,6 @@ struct ResStep {
     int32_t N, max_iter;
     ContState cs;
     ContOut co;                  // iters / valid (hard / post are written by k_var_m)
-    unsigned long long* syn_acc; // [tile][M] row parities accumulated by the variable kernel (nullptr: gather)
 };
 
 }  // namespace dev

@@ -420,12 +420,7 @@ __global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ 
             ln0 = rs.cs.lane_n[t * TILE + lane];
             b0 = rs.cs.lane_b[t * TILE + lane];
         }
-        if (row < M && !rs.syn_acc) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
-    }
-    if (SYN && rs.syn_acc && row < M) {  // accumulated by the variable kernel; consumed (re-armed) here
-        unsigned long long v = 0;
-        if (lane == 0) v = atomicExch(rs.syn_acc + (size_t)t * M + row, 0ull);
-        par = (uint64_t)__shfl(v, 0);
+        if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
     }
     if (run)
         check_bp_row<DC, NT, CSCL>(dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane,
@@ -670,18 +665,7 @@ __global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, d
             for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
         }
         const uint64_t m = __ballot(h);
-        if (CONT && rf.syn_acc) {
-            // accumulated syndrome: the stored word goes to the column's DV rows
-            const size_t o = (size_t)t * N + j;
-            const uint64_t old = (touched == ~0ull) ? 0ull : hard[o];
-            const uint64_t w = (old & ~touched) | (m & touched);
-            if (lane == 0) hard[o] = w;
-            int32_t myrow = 0;
-#pragma unroll
-            for (int s = 0; s < DV; ++s)
-                if (lane == s) myrow = eid[c][s] / rf.syn_dc;
-            if (lane < DV) atomicXor(rf.syn_acc + (size_t)t * rf.syn_m + myrow, (unsigned long long)w);
-        } else if (lane == 0) {
+        if (lane == 0) {
             const size_t o = (size_t)t * N + j;
             const uint64_t old = (touched == ~0ull) ? 0ull : hard[o];
             hard[o] = (old & ~touched) | (m & touched);

@@ -481,14 +481,10 @@ def test_split_syndrome_bitexact(gpu, og, codewords, monkeypatch, algo, msa_c, g
     _cmp(G2, og, llr[:3], 20, algo=algo, chunk=chunk)
 
 
-@pytest.mark.parametrize("algo,msa_c,tiles,split", [("bp", 0, 3, 32), ("bp", 0, 1, 5), ("msa", 0, 2, 64), ("msa", 1, 2, 16),
-                                                     ("bp", 0, 3, -1), ("bp", 0, 1, -1), ("msa", 0, 2, -1)])
+@pytest.mark.parametrize("algo,msa_c,tiles,split", [("bp", 0, 3, 32), ("bp", 0, 1, 5), ("msa", 0, 2, 64), ("msa", 1, 2, 16)])
 def test_resident_pool_split_syndrome_bitexact(gpu, og, codewords, monkeypatch, algo, msa_c, tiles, split):
     """LDPC_RES_SYN > 0: the resident pool with a separate multi-block
-    syndrome launch (k_syndrome_split) before a plain in-place check;
-    LDPC_RES_SYN = -1 (BP): row parities accumulated by the variable kernel
-    (atomic XOR of every stored ballot word into its rows) and taken by the
-    next check kernel (min-sum ignores it: fused gathers)."""
+    syndrome launch (k_syndrome_split) before a plain in-place check."""
     monkeypatch.setenv("LDPC_RES", "1")
     monkeypatch.setenv("LDPC_RES_MSA_C", "1")
     monkeypatch.setenv("LDPC_RES_SYN", str(split))
