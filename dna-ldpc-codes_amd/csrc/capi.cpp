@@ -25,53 +25,89 @@ using ldpc::Engine;
 using ldpc::HostGraph;
 using ldpc::set_error;
 
+// shards up to this many codewords get a lane pool holding all of them
+// (the 272-codeword DNA batch: 248k cw/s grouped vs 194k through the
+// resident pool); larger ones use the engine's own pool
+constexpr int64_t kExplicitPoolMax = 1024;
+constexpr int64_t kXferChunk = 4096;  // codewords per PCIe chunk (at least)
+
 namespace {
 
-// One reusable device context for host-buffer decodes.
+// One reusable device context for host-buffer decodes: an engine plus two
+// sets of pinned / device staging buffers of `xfer` codewords each, so that
+// the host-side exp and the PCIe copies of one chunk overlap the decode of
+// the previous one.  The engine decodes each chunk through its lane pool
+// (pool codewords, 0: its own choice -- the resident pool for BP), by
+// continuous refill when the chunk is larger.
 struct Slot {
     std::unique_ptr<Engine> eng;
     int device = 0, algo = 0;
-    int64_t cap = 0;
-    double* h_in = nullptr;   // pinned [cap][N]
-    double* h_post = nullptr; // pinned [cap][N]
-    uint8_t* h_hard = nullptr;
-    int32_t* h_iters = nullptr;
-    uint8_t* h_valid = nullptr;
-    double* d_in = nullptr;
-    double* d_post = nullptr;
-    uint8_t* d_hard = nullptr;
-    int32_t* d_iters = nullptr;
-    uint8_t* d_valid = nullptr;
+    int64_t pool = 0, xfer = 0;
+    hipStream_t copy = nullptr, copy_out = nullptr;  // H2D / D2H streams (the engine computes on its own)
+    hipEvent_t ev_h2d[2] = {}, ev_dec[2] = {}, ev_d2h[2] = {};
+    double* h_in[2] = {};
+    double* h_post[2] = {};
+    uint8_t* h_hard[2] = {};
+    int32_t* h_iters[2] = {};
+    uint8_t* h_valid[2] = {};
+    double* d_in[2] = {};
+    double* d_post[2] = {};
+    uint8_t* d_hard[2] = {};
+    int32_t* d_iters[2] = {};
+    uint8_t* d_valid[2] = {};
 
     ~Slot()
     {
         if (eng) hipSetDevice(device);
-        hipHostFree(h_in); hipHostFree(h_post); hipHostFree(h_hard); hipHostFree(h_iters); hipHostFree(h_valid);
-        hipFree(d_in); hipFree(d_post); hipFree(d_hard); hipFree(d_iters); hipFree(d_valid);
+        for (int k = 0; k < 2; k++) {
+            hipHostFree(h_in[k]); hipHostFree(h_post[k]); hipHostFree(h_hard[k]); hipHostFree(h_iters[k]);
+            hipHostFree(h_valid[k]);
+            hipFree(d_in[k]); hipFree(d_post[k]); hipFree(d_hard[k]); hipFree(d_iters[k]); hipFree(d_valid[k]);
+            if (ev_h2d[k]) hipEventDestroy(ev_h2d[k]);
+            if (ev_dec[k]) hipEventDestroy(ev_dec[k]);
+            if (ev_d2h[k]) hipEventDestroy(ev_d2h[k]);
+        }
+        if (copy) hipStreamDestroy(copy);
+        if (copy_out) hipStreamDestroy(copy_out);
         eng.reset();
+    }
+    // posterior staging is allocated on the first call that asks for it
+    int want_post(size_t N)
+    {
+        for (int k = 0; k < 2 && !h_post[k]; k++) {
+            LDPC_HIP(hipHostMalloc((void**)&h_post[k], (size_t)xfer * N * sizeof(double), hipHostMallocDefault));
+            LDPC_HIP(hipMalloc((void**)&d_post[k], (size_t)xfer * N * sizeof(double)));
+        }
+        return LDPC_OK;
     }
 };
 
-int make_slot(const HostGraph* g, int device, int algo, int64_t cap, std::unique_ptr<Slot>& out)
+int make_slot(const HostGraph* g, int device, int algo, int64_t pool, int64_t xfer, std::unique_ptr<Slot>& out)
 {
     auto s = std::make_unique<Slot>();
     s->device = device;
     s->algo = algo;
     s->eng = std::make_unique<Engine>();
-    int rc = s->eng->init(g, device, algo, cap);
+    int rc = s->eng->init(g, device, algo, pool);
     if (rc) return rc;
-    s->cap = s->eng->cap;
-    const size_t N = (size_t)g->N, C = (size_t)s->cap;
-    LDPC_HIP(hipHostMalloc((void**)&s->h_in, C * N * sizeof(double), hipHostMallocDefault));
-    LDPC_HIP(hipHostMalloc((void**)&s->h_post, C * N * sizeof(double), hipHostMallocDefault));
-    LDPC_HIP(hipHostMalloc((void**)&s->h_hard, C * N, hipHostMallocDefault));
-    LDPC_HIP(hipHostMalloc((void**)&s->h_iters, C * sizeof(int32_t), hipHostMallocDefault));
-    LDPC_HIP(hipHostMalloc((void**)&s->h_valid, C, hipHostMallocDefault));
-    LDPC_HIP(hipMalloc((void**)&s->d_in, C * N * sizeof(double)));
-    LDPC_HIP(hipMalloc((void**)&s->d_post, C * N * sizeof(double)));
-    LDPC_HIP(hipMalloc((void**)&s->d_hard, C * N));
-    LDPC_HIP(hipMalloc((void**)&s->d_iters, C * sizeof(int32_t)));
-    LDPC_HIP(hipMalloc((void**)&s->d_valid, C));
+    s->pool = pool;
+    s->xfer = xfer;
+    const size_t N = (size_t)g->N, C = (size_t)s->xfer;
+    LDPC_HIP(hipStreamCreateWithFlags(&s->copy, hipStreamNonBlocking));
+    LDPC_HIP(hipStreamCreateWithFlags(&s->copy_out, hipStreamNonBlocking));
+    for (int k = 0; k < 2; k++) {
+        LDPC_HIP(hipEventCreateWithFlags(&s->ev_h2d[k], hipEventDisableTiming));
+        LDPC_HIP(hipEventCreateWithFlags(&s->ev_dec[k], hipEventDisableTiming));
+        LDPC_HIP(hipEventCreateWithFlags(&s->ev_d2h[k], hipEventDisableTiming));
+        LDPC_HIP(hipHostMalloc((void**)&s->h_in[k], C * N * sizeof(double), hipHostMallocDefault));
+        LDPC_HIP(hipHostMalloc((void**)&s->h_hard[k], C * N, hipHostMallocDefault));
+        LDPC_HIP(hipHostMalloc((void**)&s->h_iters[k], C * sizeof(int32_t), hipHostMallocDefault));
+        LDPC_HIP(hipHostMalloc((void**)&s->h_valid[k], C, hipHostMallocDefault));
+        LDPC_HIP(hipMalloc((void**)&s->d_in[k], C * N * sizeof(double)));
+        LDPC_HIP(hipMalloc((void**)&s->d_hard[k], C * N));
+        LDPC_HIP(hipMalloc((void**)&s->d_iters[k], C * sizeof(int32_t)));
+        LDPC_HIP(hipMalloc((void**)&s->d_valid[k], C));
+    }
     out = std::move(s);
     return LDPC_OK;
 }
@@ -93,12 +129,17 @@ struct ldpc_graph {
     std::mutex mu;
     std::vector<std::unique_ptr<Slot>> free_slots;
 
-    std::unique_ptr<Slot> take(int device, int algo, int64_t need)
+    // a slot with the same lane pool (0: the engine's own) and staging for
+    // at least `xfer` codewords per chunk
+    // (small: any small-batch pool of at least `pool` lanes will do -- the
+    // extra tiles stay empty -- so calls of varying small sizes share one)
+    std::unique_ptr<Slot> take(int device, int algo, int64_t pool, int64_t xfer, bool small)
     {
         std::lock_guard<std::mutex> lk(mu);
         for (size_t i = 0; i < free_slots.size(); i++) {
             auto& s = free_slots[i];
-            if (s->device == device && s->algo == algo && s->cap >= need) {
+            const bool pool_ok = small ? (s->pool >= pool && s->pool <= kExplicitPoolMax) : s->pool == pool;
+            if (s->device == device && s->algo == algo && pool_ok && s->xfer >= xfer) {
                 auto r = std::move(s);
                 free_slots.erase(free_slots.begin() + (long)i);
                 return r;
@@ -276,52 +317,103 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
         const int64_t s1 = B * (int64_t)(di + 1) / (int64_t)devs.size();
         const int64_t shard = s1 - s0;
         if (shard <= 0) return;
-        int64_t chunk = o.chunk > 0 ? o.chunk : 4096;
-        chunk = std::min<int64_t>(chunk, (shard + 63) / 64 * 64);
-        std::unique_ptr<Slot> slot = g->take(dev, algo, chunk);
+        // lane pool: the caller's chunk; else for small shards (the DNA batch)
+        // one holding all of them (every codeword in flight at once), else the
+        // engine's own (0: the resident pool for BP).  Codewords move through
+        // PCIe in double-buffered chunks of `xfer`.
+        const int64_t sh64 = (shard + 63) / 64 * 64;
+        const int64_t pool = o.chunk > 0 ? o.chunk : (shard <= kExplicitPoolMax ? sh64 : 0);
+        const int64_t xfer = std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool + 63) / 64 * 64));
+        std::unique_ptr<Slot> slot = g->take(dev, algo, pool, xfer, o.chunk <= 0 && pool > 0);
         int rc = LDPC_OK;
-        if (!slot) rc = make_slot(&g->h, dev, algo, chunk, slot);
+        if (!slot) rc = make_slot(&g->h, dev, algo, pool, xfer, slot);
+        if (!rc && post_out) rc = slot->want_post(N);
         if (rc) { rcs[di] = rc; msgs[di] = ldpc::last_error(); return; }
-        Engine& E = *slot->eng;
+        Slot& S = *slot;
+        Engine& E = *S.eng;
         const bool host_exp = (algo == LDPC_ALGO_BP) && o.exp_on_host;
         const int in_kind = (algo == LDPC_ALGO_BP && host_exp) ? LDPC_IN_LR : LDPC_IN_LLR;
-        for (int64_t b0 = s0; b0 < s1 && rc == LDPC_OK; b0 += slot->cap) {
-            const int64_t Bc = std::min<int64_t>(slot->cap, s1 - b0);
-            const double* src = llr + (size_t)b0 * N;
-            if (host_exp)  // DNA_main.cpp:1344  g_received_LR[i] = exp(g_received_LLR[i])
+        const int64_t X = S.xfer, nch = (shard + X - 1) / X;
+        auto c0 = [&](int64_t c) { return s0 + c * X; };
+        auto cn = [&](int64_t c) { return std::min<int64_t>(X, s1 - c0(c)); };
+        // host side of chunk c: exp (DNA_main.cpp:1344  g_received_LR[i] =
+        // exp(g_received_LLR[i])) or copy into pinned staging, then H2D on the
+        // copy stream once the decode that last read that device buffer is done
+        auto prep = [&](int64_t c) -> int {
+            const int k = (int)(c & 1);
+            const int64_t Bc = cn(c);
+            const double* src = llr + (size_t)c0(c) * N;
+            LDPC_HIP(hipSetDevice(dev));
+            if (c >= 2) LDPC_HIP(hipEventSynchronize(S.ev_h2d[k]));  // staging buffer free again
+            if (host_exp)
                 parallel_rows(Bc, host_threads, [&](int64_t r0, int64_t r1) {
-                    for (size_t i = (size_t)r0 * N; i < (size_t)r1 * N; i++) slot->h_in[i] = std::exp(src[i]);
+                    for (size_t i = (size_t)r0 * N; i < (size_t)r1 * N; i++) S.h_in[k][i] = std::exp(src[i]);
                 });
             else
                 parallel_rows(Bc, host_threads, [&](int64_t r0, int64_t r1) {
-                    std::memcpy(slot->h_in + (size_t)r0 * N, src + (size_t)r0 * N, (size_t)(r1 - r0) * N * 8);
+                    std::memcpy(S.h_in[k] + (size_t)r0 * N, src + (size_t)r0 * N, (size_t)(r1 - r0) * N * 8);
                 });
-            auto step = [&]() -> int {
-                LDPC_HIP(hipSetDevice(dev));
-                if (algo == LDPC_ALGO_QMSA) {
-                    int r = E.set_params(q_prec, q_step, o.msa_offset, o.tie_seed);
-                    if (r) return r;
-                }
-                E.tie_base = b0;  // tie hash keyed by the codeword's index in this call
-                LDPC_HIP(hipMemcpyAsync(slot->d_in, slot->h_in, (size_t)Bc * N * 8, hipMemcpyHostToDevice, E.stream));
-                int r = E.decode(slot->d_in, in_kind, Bc, max_iter, slot->d_hard, post_out ? slot->d_post : nullptr,
-                                    o.post_kind, slot->d_iters, slot->d_valid);
+            if (c >= 2) LDPC_HIP(hipStreamWaitEvent(S.copy, S.ev_dec[k], 0));
+            LDPC_HIP(hipMemcpyAsync(S.d_in[k], S.h_in[k], (size_t)Bc * N * 8, hipMemcpyHostToDevice, S.copy));
+            LDPC_HIP(hipEventRecord(S.ev_h2d[k], S.copy));
+            return LDPC_OK;
+        };
+        // outputs of chunk c, once its D2H copies are done
+        auto finish = [&](int64_t c) -> int {
+            const int k = (int)(c & 1);
+            const int64_t b0 = c0(c), Bc = cn(c);
+            LDPC_HIP(hipEventSynchronize(S.ev_d2h[k]));
+            std::memcpy(hard_out + (size_t)b0 * N, S.h_hard[k], (size_t)Bc * N);
+            if (post_out) std::memcpy(post_out + (size_t)b0 * N, S.h_post[k], (size_t)Bc * N * 8);
+            if (iters_out) std::memcpy(iters_out + b0, S.h_iters[k], (size_t)Bc * 4);
+            if (valid_out) std::memcpy(valid_out + b0, S.h_valid[k], (size_t)Bc);
+            return LDPC_OK;
+        };
+        auto decode = [&](int64_t c) -> int {
+            const int k = (int)(c & 1);
+            const int64_t Bc = cn(c);
+            LDPC_HIP(hipSetDevice(dev));
+            if (algo == LDPC_ALGO_QMSA) {
+                int r = E.set_params(q_prec, q_step, o.msa_offset, o.tie_seed);
                 if (r) return r;
-                LDPC_HIP(hipMemcpyAsync(slot->h_hard, slot->d_hard, (size_t)Bc * N, hipMemcpyDeviceToHost, E.stream));
-                if (post_out)
-                    LDPC_HIP(hipMemcpyAsync(slot->h_post, slot->d_post, (size_t)Bc * N * 8, hipMemcpyDeviceToHost,
-                                            E.stream));
-                LDPC_HIP(hipMemcpyAsync(slot->h_iters, slot->d_iters, (size_t)Bc * 4, hipMemcpyDeviceToHost, E.stream));
-                LDPC_HIP(hipMemcpyAsync(slot->h_valid, slot->d_valid, (size_t)Bc, hipMemcpyDeviceToHost, E.stream));
-                LDPC_HIP(hipStreamSynchronize(E.stream));
-                return LDPC_OK;
-            };
-            rc = step();
-            if (rc) break;
-            std::memcpy(hard_out + (size_t)b0 * N, slot->h_hard, (size_t)Bc * N);
-            if (post_out) std::memcpy(post_out + (size_t)b0 * N, slot->h_post, (size_t)Bc * N * 8);
-            if (iters_out) std::memcpy(iters_out + b0, slot->h_iters, (size_t)Bc * 4);
-            if (valid_out) std::memcpy(valid_out + b0, slot->h_valid, (size_t)Bc);
+            }
+            E.tie_base = c0(c);  // tie hash keyed by the codeword's index in this call
+            LDPC_HIP(hipStreamWaitEvent(E.stream, S.ev_h2d[k], 0));
+            int r = E.decode(S.d_in[k], in_kind, Bc, max_iter, S.d_hard[k], post_out ? S.d_post[k] : nullptr,
+                             o.post_kind, S.d_iters[k], S.d_valid[k]);
+            if (r) return r;
+            LDPC_HIP(hipEventRecord(S.ev_dec[k], E.stream));
+            LDPC_HIP(hipStreamWaitEvent(S.copy_out, S.ev_dec[k], 0));
+            LDPC_HIP(hipMemcpyAsync(S.h_hard[k], S.d_hard[k], (size_t)Bc * N, hipMemcpyDeviceToHost, S.copy_out));
+            if (post_out)
+                LDPC_HIP(hipMemcpyAsync(S.h_post[k], S.d_post[k], (size_t)Bc * N * 8, hipMemcpyDeviceToHost,
+                                        S.copy_out));
+            LDPC_HIP(hipMemcpyAsync(S.h_iters[k], S.d_iters[k], (size_t)Bc * 4, hipMemcpyDeviceToHost, S.copy_out));
+            LDPC_HIP(hipMemcpyAsync(S.h_valid[k], S.d_valid[k], (size_t)Bc, hipMemcpyDeviceToHost, S.copy_out));
+            LDPC_HIP(hipEventRecord(S.ev_d2h[k], S.copy_out));
+            return LDPC_OK;
+        };
+        rc = prep(0);
+        for (int64_t c = 0; c < nch && rc == LDPC_OK; c++) {
+            // the next chunk's host work and H2D run on a helper thread while
+            // this thread drives the decode of chunk c
+            int rc_next = LDPC_OK;
+            std::string err_next;
+            std::thread next;
+            if (c + 1 < nch)
+                next = std::thread([&, c] {
+                    rc_next = prep(c + 1);
+                    if (rc_next) err_next = ldpc::last_error();
+                });
+            rc = decode(c);
+            if (rc == LDPC_OK && c >= 1) rc = finish(c - 1);
+            if (next.joinable()) next.join();
+            if (rc == LDPC_OK && rc_next) { rc = rc_next; set_error(err_next); }
+        }
+        if (rc == LDPC_OK) rc = finish(nch - 1);
+        if (rc == LDPC_OK && hipStreamSynchronize(E.stream) != hipSuccess) {  // surplus steps of the last decode
+            set_error("hipStreamSynchronize failed");
+            rc = LDPC_ERR_DEVICE;
         }
         if (rc) { rcs[di] = rc; msgs[di] = ldpc::last_error(); return; }
         g->give(std::move(slot));

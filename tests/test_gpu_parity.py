@@ -319,21 +319,21 @@ def test_resident_pool_in_place_bitexact(gpu, og, codewords, monkeypatch, res, t
     monkeypatch.setenv("LDPC_CONT", "1")
     G2 = gpu.Graph(PCHK)
     llr = synth.dna_like_llrs(codewords, seed=1, reads=57000)[:200]
-    _cmp(G2, og, llr, 60)
+    _cmp(G2, og, llr, 60, chunk=64 * tiles)
     llr = np.concatenate([synth.bsc_llrs(codewords, 0, 150, seed=3, p=0.003),
                           synth.bsc_llrs(codewords, 150, 130, seed=2026, p=0.02)])
-    _, _, it, _ = _cmp(G2, og, llr, 50)
+    _, _, it, _ = _cmp(G2, og, llr, 50, chunk=64 * tiles)
     assert (it[150:] == 50).all() and len(np.unique(it[:150])) > 2
-    _cmp(G2, og, llr[:70], 0)
-    _cmp(G2, og, llr[:5], 50)
-    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 200, seed=8, p=0.002), 30, algo="msa")
+    _cmp(G2, og, llr[:70], 0, chunk=64 * tiles)
+    _cmp(G2, og, llr[:5], 50, chunk=64 * tiles)
+    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 200, seed=8, p=0.002), 30, algo="msa", chunk=64 * tiles)
     rng = np.random.default_rng(21)
     llr = synth.dna_like_llrs(codewords, seed=2, reads=60000)[:100]
     llr[rng.random(llr.shape) < 0.002] = np.nan
     llr[rng.random(llr.shape) < 0.002] = np.inf
     llr[rng.random(llr.shape) < 0.002] = -np.inf
     ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 40, algo=0, post_mode=1, threads=8)
-    h, p, it, v = G2.decode(llr, max_iter=40, algo="bp", post="ratio")
+    h, p, it, v = G2.decode(llr, max_iter=40, algo="bp", post="ratio", chunk=64 * tiles)
     assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
     nan = np.isnan(ref_p)
     assert np.array_equal(np.isnan(p), nan)
@@ -403,11 +403,11 @@ def test_min_sum_compressed_resident_pool_bitexact(gpu, og, codewords, monkeypat
     monkeypatch.setenv("LDPC_CONT", "1")
     G2 = gpu.Graph(PCHK)
     llr = synth.bsc_llrs(codewords, 0, 300, seed=2026, p=0.002)
-    _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa")
+    _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", chunk=64 * tiles)
     assert len(np.unique(it)) > 2
-    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 70, seed=5, p=0.01), 12, algo="msa")
-    _cmp(G2, og, llr[:70], 0, algo="msa")
-    _cmp(G2, og, llr[:5], 50, algo="msa")
+    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 70, seed=5, p=0.01), 12, algo="msa", chunk=64 * tiles)
+    _cmp(G2, og, llr[:70], 0, algo="msa", chunk=64 * tiles)
+    _cmp(G2, og, llr[:5], 50, algo="msa", chunk=64 * tiles)
     rng = np.random.default_rng(17)
     llr = synth.bsc_llrs(codewords, 0, 130, seed=11, p=0.004)
     llr[rng.random(llr.shape) < 0.003] = np.nan
@@ -416,7 +416,7 @@ def test_min_sum_compressed_resident_pool_bitexact(gpu, og, codewords, monkeypat
     llr[rng.random(llr.shape) < 0.01] = -0.0
     llr[:2] = np.nan
     ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 20, algo=1, post_mode=0, threads=8)
-    h, p, it, v = G2.decode(llr, max_iter=20, algo="msa", post="llr")
+    h, p, it, v = G2.decode(llr, max_iter=20, algo="msa", post="llr", chunk=64 * tiles)
     assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
     nan = np.isnan(ref_p)
     assert np.array_equal(np.isnan(p), nan)
@@ -496,10 +496,10 @@ def test_resident_pool_split_syndrome_bitexact(gpu, og, codewords, monkeypatch, 
     if algo == "bp":
         llr = np.concatenate([synth.bsc_llrs(codewords, 0, 200, seed=3, p=0.003),
                               synth.bsc_llrs(codewords, 200, 100, seed=2026, p=0.02)])
-        _, _, it, _ = _cmp(G2, og, llr, 30)
+        _, _, it, _ = _cmp(G2, og, llr, 30, chunk=64 * tiles)
     else:
         llr = synth.bsc_llrs(codewords, 0, 300, seed=2026, p=0.002)
-        _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa")
+        _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", chunk=64 * tiles)
     assert len(np.unique(it)) > 2
-    _cmp(G2, og, llr[:70], 0, algo=algo)
-    _cmp(G2, og, llr[:3], 20, algo=algo)
+    _cmp(G2, og, llr[:70], 0, algo=algo, chunk=64 * tiles)
+    _cmp(G2, og, llr[:3], 20, algo=algo, chunk=64 * tiles)
