@@ -74,7 +74,10 @@ typedef struct ldpc_graph ldpc_graph;
 typedef struct ldpc_opts {
     int32_t n_devices;      /* <= 0: use device 0 only */
     const int32_t *devices; /* device ordinals (NULL: 0..n_devices-1) */
-    int64_t chunk;          /* codewords resident per device per pass (0: auto) */
+    int64_t chunk;          /* lane pool: codewords resident per device at once (0: auto --
+                               all of a shard of <= 1024, else the engine's own pool);
+                               codewords cross PCIe in double-buffered chunks of
+                               max(4096, chunk) that overlap the decode */
     int32_t exp_on_host;    /* BP: compute LR = exp(LLR) with the host libm, exactly as
                                DNA_main.cpp:1344 does (default 1 when opts == NULL) */
     int32_t post_kind;      /* LDPC_POST_* */
