@@ -462,7 +462,7 @@ int ldpc_engine_info(ldpc_engine* e, int64_t* cap, int64_t* group_tiles, int32_t
     if (group_tiles) *group_tiles = e->e->group_tiles;
     if (flags) *flags = (e->e->nt_d ? 1 : 0) | (e->e->pipe ? 2 : 0) | (e->e->lr_csc ? 4 : 0) | (e->e->cont ? 8 : 0) |
                         (e->e->msa_c ? 16 : 0) | (e->e->res ? 32 : 0) | (e->e->syn_split ? 64 : 0) |
-                        (e->e->syn_fused ? 128 : 0);
+                        (e->e->syn_fused ? 128 : 0) | (e->e->res && e->e->tile_streams ? 256 : 0);
     return LDPC_OK;
 }
 
@@ -499,7 +499,19 @@ int ldpc_engine_profile(ldpc_engine* e, int32_t stride)
     int rc = e->e->collect_stats();
     if (rc) return rc;
     for (int c = 0; c < ldpc::K_NCLASS; c++) { e->e->launches[c] = 0; e->e->ms[c] = 0; e->e->sampled[c] = 0; }
+    e->e->wall_ms = 0;
+    e->e->wall_runs = 0;
     e->e->profile_stride = stride > 0 ? stride : 0;
+    return LDPC_OK;
+}
+
+int ldpc_engine_wall(ldpc_engine* e, double* ms, int64_t* runs)
+{
+    if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
+    int rc = e->e->collect_stats();
+    if (rc) return rc;
+    if (ms) *ms = e->e->wall_ms;
+    if (runs) *runs = e->e->wall_runs;
     return LDPC_OK;
 }
 

@@ -57,6 +57,14 @@ struct Engine {
     int32_t* d_fin_n = nullptr;             // res: [tile*64] their iteration count
     const dev::ResStep* rstep = nullptr;    // res: set around the check launch of a step
     static constexpr int kRing = 8, kLag = 2;
+    // res with tile_streams: one stream per pool tile (LDPC_RES_STREAMS)
+    static constexpr int kMaxTileStreams = 4;
+    int tile_streams = 0;  // 0 off, 1 on, 2 staggered start, 3 re-staggered at every poll step
+    hipStream_t tstream[kMaxTileStreams] = {};
+    hipEvent_t ev_tjoin[kMaxTileStreams] = {};
+    hipEvent_t ev_tring[kRing][kMaxTileStreams] = {};
+    unsigned long long* d_occ_t = nullptr;  // [kRing][kMaxTileStreams] per-tile occupancy counters
+    unsigned long long* h_occ_t = nullptr;
     uint64_t* d_fresh = nullptr;
     uint64_t* d_occ = nullptr;
     int64_t* d_lane_b = nullptr;
@@ -95,6 +103,12 @@ struct Engine {
     std::vector<hipEvent_t> ev_pool;
     int64_t launches[K_NCLASS] = {0};
     double ms[K_NCLASS] = {0};
+    // whole continuous decodes with concurrent tile streams (HIP events on
+    // `stream` around each run while profiling): their kernels overlap, so
+    // the roofline of the concurrent set is bytes / this wall time
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> wall_live;
+    double wall_ms = 0;
+    int64_t wall_runs = 0;
 
     ~Engine();
     int init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, int64_t group = -1, int nt = -1,

@@ -68,7 +68,7 @@ EXPORTS = [
     "ldpc_graph_load_alist", "ldpc_graph_rs_ldpc", "ldpc_graph_save_pchk", "ldpc_graph_save_alist",
     "ldpc_graph_free", "ldpc_graph_info", "ldpc_graph_edges", "ldpc_graph_syndrome", "ldpc_decode",
     "ldpc_engine_create", "ldpc_engine_create_ex", "ldpc_engine_info", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
-    "ldpc_engine_gen_bsc", "ldpc_engine_set_params", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
+    "ldpc_engine_gen_bsc", "ldpc_engine_set_params", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_engine_wall", "ldpc_dev_malloc", "ldpc_dev_free",
     "ldpc_dev_memcpy", "ldpc_dna_llr", "ldpc_dna_edit_distance", "ldpc_write_soft_files", "ldpc_py_float_repr",
 ]
 
@@ -119,6 +119,7 @@ def lib():
         L.ldpc_engine_profile.argtypes = [vp, i32]
         L.ldpc_engine_set_params.argtypes = [vp, i32, dbl, i32, C.c_uint64]
         L.ldpc_engine_stats.argtypes = [vp, C.POINTER(KernelStats)]
+        L.ldpc_engine_wall.argtypes = [vp, vp, vp]
         L.ldpc_dev_malloc.argtypes = [i32, C.c_size_t]
         L.ldpc_dev_malloc.restype = vp
         L.ldpc_dev_free.argtypes = [i32, vp]
@@ -431,6 +432,7 @@ class Engine:
         self.resident = bool(fl.value & 32)  # in-place pool of a few tiles (LDPC_RES)
         self.syndrome_split = bool(fl.value & 64)  # multi-block continuous-mode syndrome (LDPC_SYN_SPLIT)
         self.syndrome_fused = bool(fl.value & 128)  # syndrome in the grouped check launches (LDPC_SYN_FUSED)
+        self.tile_streams = bool(fl.value & 256)  # resident pool, one stream per tile (LDPC_RES_STREAMS)
 
     def decode(self, d_in, in_kind: int, B: int, max_iter: int, d_hard=None, d_post=None, post_kind=POST_LLR,
                d_iters=None, d_valid=None):
@@ -450,6 +452,12 @@ class Engine:
     def profile(self, stride: int):
         """HIP-event timing of every `stride`-th launch per kernel class (0: off)."""
         _check(lib().ldpc_engine_profile(self._h, int(stride)))
+
+    def wall(self):
+        """(ms, runs): device time of whole decodes with concurrent tile streams."""
+        ms, runs = C.c_double(), C.c_int64()
+        _check(lib().ldpc_engine_wall(self._h, C.byref(ms), C.byref(runs)))
+        return ms.value, runs.value
 
     def stats(self) -> dict:
         s = KernelStats()

@@ -219,9 +219,15 @@ int ldpc_engine_set_params(ldpc_engine *e, int32_t msa_precision, double msa_ste
  * messages (env LDPC_MSA_C); bit 5 as in create_ex; bit 6 =
  * continuous-mode syndrome spread over several blocks per tile (env
  * LDPC_SYN_SPLIT); bit 7 = syndrome fused into the grouped check launches
- * (env LDPC_SYN_FUSED). */
+ * (env LDPC_SYN_FUSED); bit 8 = resident pool with one HIP stream per pool
+ * tile (env LDPC_RES_STREAMS; the tiles' kernels run concurrently). */
 int ldpc_engine_info(ldpc_engine *e, int64_t *cap, int64_t *group_tiles, int32_t *flags);
 int ldpc_engine_stats(ldpc_engine *e, ldpc_kernel_stats *out);
+/* Device time of whole decodes with concurrent tile streams (bit 8 of
+ * ldpc_engine_info): HIP events on the engine stream around each decode
+ * while profiling is on (ldpc_engine_profile resets it).  Their kernels
+ * overlap, so per-launch durations do not add up to the decode's time. */
+int ldpc_engine_wall(ldpc_engine *e, double *ms, int64_t *runs);
 
 /* Device buffers for callers without their own HIP allocator (bench, tests). */
 enum { LDPC_H2D = 0, LDPC_D2H = 1, LDPC_D2D = 2 };

@@ -503,3 +503,27 @@ def test_resident_pool_split_syndrome_bitexact(gpu, og, codewords, monkeypatch, 
     assert len(np.unique(it)) > 2
     _cmp(G2, og, llr[:70], 0, algo=algo, chunk=64 * tiles)
     _cmp(G2, og, llr[:3], 20, algo=algo, chunk=64 * tiles)
+
+
+@pytest.mark.parametrize("algo,tiles,mode", [("bp", 3, 1), ("bp", 2, 2), ("bp", 1, 1), ("msa", 3, 2), ("bp", 3, 2), ("bp", 3, 3), ("msa", 2, 3)])
+def test_resident_pool_tile_streams_bitexact(gpu, og, codewords, monkeypatch, algo, tiles, mode):
+    """LDPC_RES_STREAMS: the resident pool with one HIP stream per pool tile
+    (independent check/variable chains, per-tile occupancy counters, a join
+    back into the engine stream at the end).  Pools of 1-3 tiles with refills,
+    mixed exits, max_iter 0 and batches smaller than the pool."""
+    monkeypatch.setenv("LDPC_RES", "1")
+    monkeypatch.setenv("LDPC_RES_STREAMS", str(mode))
+    monkeypatch.setenv("LDPC_MSA_C", "0")
+    monkeypatch.setenv("LDPC_CONT", "1")
+    G2 = gpu.Graph(PCHK)
+    if algo == "bp":
+        llr = np.concatenate([synth.bsc_llrs(codewords, 0, 200, seed=3, p=0.003),
+                              synth.bsc_llrs(codewords, 200, 100, seed=2026, p=0.02)])
+        _, _, it, _ = _cmp(G2, og, llr, 30, chunk=64 * tiles)
+        _cmp(G2, og, synth.dna_like_llrs(codewords, seed=1, reads=57000)[:150], 60, chunk=64 * tiles)
+    else:
+        llr = synth.bsc_llrs(codewords, 0, 300, seed=2026, p=0.002)
+        _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", chunk=64 * tiles)
+    assert len(np.unique(it)) > 2
+    _cmp(G2, og, llr[:70], 0, algo=algo, chunk=64 * tiles)
+    _cmp(G2, og, llr[:3], 20, algo=algo, chunk=64 * tiles)
