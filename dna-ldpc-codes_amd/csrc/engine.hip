@@ -46,7 +46,7 @@ constexpr int64_t kDefaultRes = 1;       // LDPC_RES: resident in-place pool for
 constexpr int64_t kDefaultResTiles = 3;  // LDPC_RES_TILES: pool tiles (3 x 85 MB ~ the 256 MB Infinity Cache; A/B)
 constexpr int64_t kDefaultResPoll = 8;
 constexpr int64_t kResAutoMaxTiles = 4;      // explicit pools above this many tiles: grouped schedule unless LDPC_RES is set
-constexpr int64_t kDefaultResStreams = 1;    // LDPC_RES_STREAMS: resident pool, one HIP stream per pool tile (fresh-rotation A/B: 26.17k -> 28.04k cw/s)
+constexpr int64_t kDefaultResStreams = 0;    // LDPC_RES_STREAMS: resident pool, one HIP stream per pool tile (bimodal 25.1-28.4k vs 25.7-26.2k single-stream; neutral in bench.py, so off)
 constexpr int64_t kDefaultResSyn = 0;        // LDPC_RES_SYN: resident pool syndrome, 0 = fused into the check kernel, >0 = k_syndrome_split blocks per tile
 constexpr int64_t kDefaultSynSplit = 32;     // LDPC_SYN_SPLIT: syndrome blocks per tile in continuous mode (0: one block, k_syndrome_cont; A/B min-sum config 5 +5-6 %)
 constexpr int64_t kDefaultSynFused = 0;      // LDPC_SYN_FUSED: grouped continuous mode, syndrome fused into the check kernel
