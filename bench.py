@@ -5,9 +5,11 @@ iterations (BASELINE.json metric), one process per GPU.
     python bench.py                       # N=1, 100k synthetic codewords per step
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Workload (SURVEY 8(d) config 3, weak-scaled per GPU for configs 4): every
+Workload (SURVEY 8(d) config 3, weak-scaled per GPU by default): every
 rank decodes its own contiguous shard of `--batch-per-gpu` codewords
-[rank*B, (rank+1)*B) from the counter-based BSC(p=0.02) generator (transmitted
+[rank*B, (rank+1)*B) -- or, with `--global-batch G` (config 4: `--gpus 8
+--global-batch 1000000`), its dist.shard of [0, G), "scaling": "strong" --
+from the counter-based BSC(p=0.02) generator (transmitted
 word codeword_n18432_m1860_{1 + b mod 272}, LLR = +-ln49, LR = exp(LLR) by the
 host libm as DNA_main.cpp:1344 does).  p = 0.02 never converges, so every
 codeword runs exactly 50 iterations.  Inputs are generated into HBM before the
@@ -17,6 +19,11 @@ check, variable], final syndrome, hard-bit unpack, iteration counts).
 No data-path collective: ranks only meet in a barrier and a MAX of their
 elapsed times (gloo, CPU tensors).  `value` = all codewords of all ranks /
 max elapsed.
+
+Correctness of the timed decode: at N = 1 the cpu_baseline leg decodes a
+sample of the same workload with the oracle and compares hard bits,
+iteration counts and valid flags of every sampled codeword with the GPU's
+(`check` in the JSON line); any mismatch exits non-zero.
 """
 from __future__ import annotations
 
@@ -42,7 +49,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch-per-gpu", type=int, default=100_000)
+    ap.add_argument("--batch-per-gpu", type=int, default=100_000,
+                    help="weak scaling: codewords per rank, rank r decodes [r*B, (r+1)*B)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: this many codewords split over the ranks by dist.shard (SURVEY 8(d) "
+                         "config 4: --gpus 8 --global-batch 1000000 -> 125k per rank); 0 = weak scaling")
+    ap.add_argument("--dump-dir", default="",
+                    help="write each rank's outputs (shard start/size, iterations, valid flags, packed hard bits) "
+                         "to <dir>/rank<r>.npz (tests)")
     ap.add_argument("--max-iter", type=int, default=50)
     ap.add_argument("--algo", default="bp", choices=["bp", "msa"])
     ap.add_argument("--p", type=float, default=0.02)
@@ -130,9 +144,13 @@ def bench_dna272(args):
     print(json.dumps(out), flush=True)
 
 
-def cpu_baseline(args, llr_fn, N):
+def cpu_baseline(args, llr_fn, N, B, gpu_out):
     """The oracle (bit-exact C restatement of dec.cpp, 'port') on the host cores,
-    on a bounded sample of the same workload."""
+    on a bounded sample of the same workload -- and the check of the timed
+    GPU decode: the oracle's hard bits, iteration counts and valid flags of
+    every sampled codeword must equal the GPU's (gpu_out(start, n) -> the
+    GPU's (hard[n][N], iters[n], valid[n]) of shard rows start..start+n-1).
+    Returns (cpu_baseline dict, check dict)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     og = oracle.OracleGraph(os.path.join(ROOT, "tests", "golden", "decode_n18432_m2048_final.pchk"))
@@ -140,24 +158,44 @@ def cpu_baseline(args, llr_fn, N):
         threads = len(os.sched_getaffinity(0))
     except AttributeError:
         threads = os.cpu_count() or 1
-    threads = max(1, min(threads, 16))
+    avail = threads
+    threads = max(1, min(threads, 16))  # the box's CPU share for one GPU (16)
     algo = 0 if args.algo == "bp" else 1
+    checked, bad = 0, []
+
+    def check(start, n, res):
+        nonlocal checked
+        rh, _, rit, rv = res
+        h, it, v = gpu_out(start, n)
+        for k in range(n):
+            if not (np.array_equal(h[k], rh[k]) and it[k] == rit[k] and bool(v[k]) == bool(rv[k])):
+                bad.append(start + k)
+        checked += n
+
     # calibrate with one codeword per thread, then size the sample for ~cpu_seconds
-    llr = llr_fn(0, threads)
+    n0 = min(threads, B)
+    llr = llr_fn(0, n0)
     t = time.perf_counter()
-    og.decode_batch(llr, args.max_iter, algo=algo, threads=threads, want_post=False)
+    check(0, n0, og.decode_batch(llr, args.max_iter, algo=algo, threads=threads, want_post=False))
     t1 = time.perf_counter() - t
     per_round = max(t1, 1e-3)
     rounds = max(1, int(args.cpu_seconds / per_round))
-    n = threads * rounds
-    llr = llr_fn(threads, n)
+    n = max(1, min(threads * rounds, B - n0))
+    start = n0 if B > n0 else 0
+    llr = llr_fn(start, n)
     t = time.perf_counter()
-    og.decode_batch(llr, args.max_iter, algo=algo, threads=threads, want_post=False)
+    res = og.decode_batch(llr, args.max_iter, algo=algo, threads=threads, want_post=False)
     el = time.perf_counter() - t
-    return {"value": round(n / el, 3), "unit": "codewords/s", "cores": threads, "kind": "port",
-            "per_core": round(n / el / threads, 3),
-            "sample": f"{n} codewords of the same BSC(p={args.p}) workload (indices {threads}..{threads + n - 1}), "
-                      f"{args.max_iter} iters, oracle/ldpc_oracle.c on {threads} host threads, {el:.1f} s"}
+    check(start, n, res)
+    cb = {"value": round(n / el, 3), "unit": "codewords/s", "cores": threads, "kind": "port",
+          "per_core": round(n / el / threads, 3),
+          "sample": f"{n} codewords of the same BSC(p={args.p}) workload (indices {start}..{start + n - 1}), "
+                    f"{args.max_iter} iters, oracle/ldpc_oracle.c on {threads} host threads "
+                    f"({avail} available, capped at the box's 16-core share), {el:.1f} s"}
+    chk = {"checked": checked, "mismatches": len(bad), "first_mismatches": bad[:8],
+           "what": "hard bits, iteration counts and valid flags of the timed GPU decode vs the oracle, "
+                   "on every codeword of the cpu_baseline sample"}
+    return cb, chk
 
 
 def main():
@@ -168,12 +206,27 @@ def main():
     import dist
     grp = dist.Group.from_env()  # gloo control plane only: barrier + MAX/SUM of scalars
     world, rank, local = grp.world, grp.rank, grp.local
+    if args.gpus != world and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: measuring {world} process(es); launch N "
+              "ranks with python -m torch.distributed.run --nproc-per-node N", file=sys.stderr, flush=True)
     import ldpc_amd as L
     import synth
 
     G = L.Graph(synth.PCHK)
     N, E = G.N, G.E
-    B = args.batch_per_gpu
+    if args.global_batch > 0:
+        # strong scaling: this rank's contiguous shard of the global range
+        # (DNA_main.cpp:629-651 Set_FrameNum's split), sizes differ by <= 1
+        b0, B = dist.shard(args.global_batch, world, rank)
+        per_rank = [dist.shard(args.global_batch, world, r)[1] for r in range(world)]
+        scaling = "strong"
+    else:
+        B = args.batch_per_gpu
+        b0 = rank * B  # weak scaling: this rank's contiguous shard of the global codeword range
+        per_rank = [B] * world
+        scaling = "weak"
+    if B <= 0:
+        raise SystemExit(f"rank {rank}: empty shard")
     # one GPU per local rank; ranks share devices round-robin when there are
     # fewer GPUs than ranks (rehearsals on a one-GPU box)
     dev = local % max(1, L.device_count())
@@ -187,7 +240,6 @@ def main():
     d_cw.upload(cw)
     in_kind = L.IN_LR if algo == "bp" else L.IN_LLR
     d_in = L.DeviceBuffer(dev, B * N * 8)
-    b0 = rank * B  # this rank's contiguous shard of the global codeword range
     eng.gen_bsc(d_in.at(0), in_kind, b0, B, d_cw.at(0), cw.shape[0], args.seed, args.p, synth.LLR_UNIT)
     d_hard = L.DeviceBuffer(dev, B * N)
     d_iters = L.DeviceBuffer(dev, B * 4)
@@ -220,6 +272,11 @@ def main():
     valid = d_valid.download(np.empty(B, np.uint8))
     total_cw = grp.sum(float(B * args.steps))
     value = total_cw / el_max
+    if args.dump_dir:
+        os.makedirs(args.dump_dir, exist_ok=True)
+        hard = d_hard.download(np.empty((B, N), np.uint8))
+        np.savez(os.path.join(args.dump_dir, f"rank{rank}.npz"), b0=b0, B=B, world=world, iters=iters, valid=valid,
+                 hard=np.packbits(hard, axis=1))
 
     # ---- roofline of the dominant kernel (algorithmic bytes) ----
     cw_iters = float(iters.sum()) * args.steps  # executed codeword-iterations (this rank)
@@ -282,6 +339,8 @@ def main():
                 break
     roof = {
         "bound": "hbm", "kernel": kname,
+        "bound_detail": "memory: HBM plus Infinity Cache (the resident pool is sized to the 256 MB cache; "
+                        "PMC DRAM vs fabric bytes in profiles/), vector-memory issue limited; no MFMA",
         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,
         "traffic_source": traffic_src,
@@ -295,10 +354,12 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "codewords/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(el_max / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": f"bsc-p{args.p}-{B // 1000}k-per-gpu-{algo}{args.max_iter}",
+        "scaling": scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": (f"bsc-p{args.p}-{args.global_batch // 1000}k-global-{algo}{args.max_iter}"
+                                if args.global_batch > 0 else f"bsc-p{args.p}-{B // 1000}k-per-gpu-{algo}{args.max_iter}"),
                    "code": "decode_n18432_m2048_final.pchk (8,72)-regular, E=147456",
-                   "batch_per_gpu": B, "global_batch": int(total_cw / args.steps), "max_iter": args.max_iter,
+                   "batch_per_gpu": B, "per_rank": per_rank, "global_batch": int(round(total_cw / args.steps)),
+                   "max_iter": args.max_iter,
                    "algo": algo, "parallelism": f"dp{world} (contiguous codeword shards, no collective)",
                    "resident_per_pass": eng.cap, "group_tiles": eng.group_tiles, "nontemporal_d": eng.nontemporal,
                    "two_stream": eng.pipeline, "continuous": eng.continuous, "resident_pool": eng.resident,
@@ -306,13 +367,22 @@ def main():
                    "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 4)},
         "roofline": roof,
     }
+    mismatches = 0
     if rank == 0 and world == 1 and args.cpu_baseline:
         def llr_fn(start, n):
             return synth.bsc_llrs(cw, b0 + start, n, seed=args.seed, p=args.p)
-        out["cpu_baseline"] = cpu_baseline(args, llr_fn, N)
+
+        def gpu_out(start, n):
+            h = d_hard.download(np.empty((n, N), np.uint8), offset=start * N)
+            return h, iters[start:start + n], valid[start:start + n]
+        out["cpu_baseline"], out["check"] = cpu_baseline(args, llr_fn, N, B, gpu_out)
+        mismatches = out["check"]["mismatches"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     grp.close()
+    if mismatches:
+        print(f"bench.py: {mismatches} codewords of the timed decode differ from the oracle", file=sys.stderr)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

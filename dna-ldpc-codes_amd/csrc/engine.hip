@@ -207,6 +207,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         for (size_t q = 0; q < g->col_edge.size(); q++) pos[(size_t)g->col_edge[q]] = (int32_t)q;
         if ((rc = upload(&d_csc_pos, pos))) return rc;
     }
+    debug_no_drain = env_int("LDPC_DEBUG_NO_DRAIN", 0) != 0;
     var_cpw = (int)env_int("LDPC_VAR_CPW", kDefaultVarCpw);
     full_lanes = (int)env_int("LDPC_FULL_LANES", kDefaultFullLanes);
     if (var_cpw != 1 && var_cpw != 2 && var_cpw != 4 && var_cpw != 8) var_cpw = 1;
@@ -472,18 +473,19 @@ int Engine::collect_stats()
     } while (0)
 #define LAUNCH(cls, ...) LAUNCH_ON(stream, cls, __VA_ARGS__)
 
-// check phase of tiles t0 .. t0+gt-1 into `scratch` (that group's c2v)
-template <bool NT, bool CSCL>
+// check phase of tiles t0 .. t0+gt-1 into `scratch` (that group's c2v;
+// INPLACE: scratch == v2c, the resident pool)
+template <bool NT, bool CSCL, bool INPLACE>
 static void check_regular(int algo, hipStream_t s, dim3 grid, const double* v2c, double* scratch, const uint64_t* active,
                           const int32_t* pos, int32_t M, int64_t E, int64_t t0, int full)
 {
     using namespace dev;
     if (algo == LDPC_ALGO_BP)
-        hipLaunchKernelGGL((k_check_bp<72, NT, CSCL, false>), grid, dim3(256), 0, s, v2c, scratch, active, pos, M, E,
-                           t0, full, ResStep{});
+        hipLaunchKernelGGL((k_check_bp<72, NT, CSCL, false, INPLACE>), grid, dim3(256), 0, s, v2c, scratch, active, pos,
+                           M, E, t0, full, ResStep{});
     else
-        hipLaunchKernelGGL((k_check_msa<72, NT, CSCL, false>), grid, dim3(256), 0, s, v2c, scratch, active, pos, M, E,
-                           t0, full, ResStep{});
+        hipLaunchKernelGGL((k_check_msa<72, NT, CSCL, false, INPLACE>), grid, dim3(256), 0, s, v2c, scratch, active,
+                           pos, M, E, t0, full, ResStep{});
 }
 
 template <bool NT, bool CSCL, bool CONT>
@@ -500,41 +502,44 @@ static void var_regular3(int algo, hipStream_t s, dim3 grid, const double* scrat
                            col_edge, pt, N, E, t0, rf);
 }
 
-template <bool MSA, bool NT, int CPW>
+template <bool MSA, bool NT, int CPW, bool INPLACE>
 static void var_multi2(hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior, uint64_t* hard,
                        const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E, int64_t t0,
                        const dev::Refill& rf, int full)
 {
     using namespace dev;
     if (rf.fresh)
-        hipLaunchKernelGGL((k_var_m<MSA, 8, NT, true, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
-                           col_edge, pt, N, E, t0, rf, full);
+        hipLaunchKernelGGL((k_var_m<MSA, 8, NT, true, CPW, INPLACE>), grid, dim3(256), 0, s, scratch, v2c, prior, hard,
+                           active, col_edge, pt, N, E, t0, rf, full);
     else
-        hipLaunchKernelGGL((k_var_m<MSA, 8, NT, false, CPW>), grid, dim3(256), 0, s, scratch, v2c, prior, hard, active,
-                           col_edge, pt, N, E, t0, rf, full);
+        hipLaunchKernelGGL((k_var_m<MSA, 8, NT, false, CPW, INPLACE>), grid, dim3(256), 0, s, scratch, v2c, prior, hard,
+                           active, col_edge, pt, N, E, t0, rf, full);
 }
 
-template <bool MSA, bool NT>
+template <bool MSA, bool NT, bool INPLACE>
 static void var_multi1(int cpw, hipStream_t s, dim3 grid, const double* scratch, double* v2c, double* prior,
                        uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E,
                        int64_t t0, const dev::Refill& rf, int full)
 {
-    if (cpw == 1) var_multi2<MSA, NT, 1>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
-    else if (cpw == 2) var_multi2<MSA, NT, 2>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
-    else if (cpw == 4) var_multi2<MSA, NT, 4>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
-    else var_multi2<MSA, NT, 8>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    if (cpw == 1) var_multi2<MSA, NT, 1, INPLACE>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    else if (cpw == 2) var_multi2<MSA, NT, 2, INPLACE>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    else if (cpw == 4) var_multi2<MSA, NT, 4, INPLACE>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+    else var_multi2<MSA, NT, 8, INPLACE>(s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
 }
 
-static void var_multi(int algo, bool nt, int cpw, hipStream_t s, dim3 grid, const double* scratch, double* v2c,
-                      double* prior, uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt,
-                      int32_t N, int64_t E, int64_t t0, const dev::Refill& rf, int full)
+// inplace: scratch == v2c (the resident pool, never nontemporal)
+static void var_multi(int algo, bool nt, bool inplace, int cpw, hipStream_t s, dim3 grid, const double* scratch,
+                      double* v2c, double* prior, uint64_t* hard, const uint64_t* active, const int32_t* col_edge,
+                      double* pt, int32_t N, int64_t E, int64_t t0, const dev::Refill& rf, int full)
 {
     if (algo == LDPC_ALGO_MSA) {
-        if (nt) var_multi1<true, true>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
-        else var_multi1<true, false>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+        if (inplace) var_multi1<true, false, true>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+        else if (nt) var_multi1<true, true, false>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+        else var_multi1<true, false, false>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
     } else {
-        if (nt) var_multi1<false, true>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
-        else var_multi1<false, false>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+        if (inplace) var_multi1<false, false, true>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+        else if (nt) var_multi1<false, true, false>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
+        else var_multi1<false, false, false>(cpw, s, grid, scratch, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf, full);
     }
 }
 
@@ -578,6 +583,9 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
     const int64_t E = g->E;
     const bool reg72 = g->regular_dc && g->dc_max == 72;
     const dim3 grid((M + 3) / 4, gt), blk(256);
+    // the resident pool writes the check messages over the variable messages
+    const bool inplace = scratch == v2c;
+    if (inplace && (msa_c || !reg72)) { set_error("in-place check phase needs the regular fp64 kernels"); return LDPC_ERR_ARG; }
     if ((res || syn_fused) && rstep) {  // syndrome + lane bookkeeping fused (ResStep)
         if (msa_c && nt_d)
             LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa_c<72, true, true>), grid, blk, 0, s, v2c,
@@ -587,11 +595,17 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
             LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa_c<72, false, true>), grid, blk, 0, s, v2c,
                                                      msa_codes(scratch), msa_rec(scratch, c2v_tiles, E), active, M, E,
                                                      t0, full_lanes, *rstep));
+        else if (algo == LDPC_ALGO_BP && inplace)
+            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_bp<72, false, false, true, true>), grid, blk, 0, s, v2c,
+                                                     scratch, active, d_csc_pos, M, E, t0, full_lanes, *rstep));
         else if (algo == LDPC_ALGO_BP)
-            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_bp<72, false, false, true>), grid, blk, 0, s, v2c, scratch,
-                                                     active, d_csc_pos, M, E, t0, full_lanes, *rstep));
+            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_bp<72, false, false, true, false>), grid, blk, 0, s, v2c,
+                                                     scratch, active, d_csc_pos, M, E, t0, full_lanes, *rstep));
+        else if (inplace)
+            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa<72, false, false, true, true>), grid, blk, 0, s, v2c,
+                                                     scratch, active, d_csc_pos, M, E, t0, full_lanes, *rstep));
         else
-            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa<72, false, false, true>), grid, blk, 0, s, v2c,
+            LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL((k_check_msa<72, false, false, true, false>), grid, blk, 0, s, v2c,
                                                      scratch, active, d_csc_pos, M, E, t0, full_lanes, *rstep));
         return LDPC_OK;
     }
@@ -608,10 +622,11 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
     }
     if (reg72) {
         LAUNCH_ON(s, K_CHECK, {
-            if (nt_d && lr_csc) check_regular<true, true>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0, full_lanes);
-            else if (nt_d) check_regular<true, false>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0, full_lanes);
-            else if (lr_csc) check_regular<false, true>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0, full_lanes);
-            else check_regular<false, false>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0, full_lanes);
+            if (inplace) check_regular<false, false, true>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0, full_lanes);
+            else if (nt_d && lr_csc) check_regular<true, true, false>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0, full_lanes);
+            else if (nt_d) check_regular<true, false, false>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0, full_lanes);
+            else if (lr_csc) check_regular<false, true, false>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0, full_lanes);
+            else check_regular<false, false, false>(algo, s, grid, v2c, scratch, active, d_csc_pos, M, E, t0, full_lanes);
         });
     } else if (algo == LDPC_ALGO_BP) {
         LAUNCH_ON(s, K_CHECK, hipLaunchKernelGGL(k_check_bp_gen, grid, blk, 0, s, v2c, scratch, active, d_row_ptr, M, E, t0));
@@ -647,10 +662,14 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         });
         return LDPC_OK;
     }
-    // (the resident pool always takes k_var_m: it writes the finished lanes' outputs)
-    if (reg8 && (res || syn_fused || syn_split || (var_cpw > 1 && nt_d)) && !lr_csc && N % (4 * var_cpw) == 0) {
+    // (the resident pool always takes k_var_m: it writes the finished lanes'
+    // outputs, and it is the only variable kernel with an in-place form)
+    const bool inplace = scratch == v2c;
+    const bool multi = reg8 && (res || syn_fused || syn_split || (var_cpw > 1 && nt_d)) && !lr_csc && N % (4 * var_cpw) == 0;
+    if (inplace && !multi) { set_error("in-place variable phase needs k_var_m"); return LDPC_ERR_ARG; }
+    if (multi) {
         const dim3 gm((unsigned)(N / (4 * var_cpw)), gt);
-        LAUNCH_ON(s, K_VAR, var_multi(algo, nt_d, var_cpw, s, gm, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf, full_lanes));
+        LAUNCH_ON(s, K_VAR, var_multi(algo, nt_d, inplace, var_cpw, s, gm, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf, full_lanes));
         return LDPC_OK;
     }
     if (reg8) {
@@ -871,6 +890,25 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     const Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0};
     const bool reg_rowT = d_col_idx_T != nullptr;
     const int hard_vec = ((uintptr_t)d_hard % 8 == 0 && N % 8 == 0) ? 1 : 0;
+    // Host step bound.  A lane finishes its codeword at most max_iter + 2
+    // steps after claiming it (refill step, max_iter iterations, the final
+    // syndrome), so within every window of max_iter + 2 steps each lane either
+    // finishes a codeword or has found the input drained; after
+    // ceil(B / lanes) + 1 windows every lane is empty.  The host reads the
+    // occupancy up to kLag polls late.  A decode still running past the bound
+    // means broken device bookkeeping: stop enqueueing and report it instead
+    // of spinning.  LDPC_DEBUG_NO_DRAIN=1 ignores the drained reading (tests).
+    const int64_t lanes = tiles * 64;
+    const int64_t windows = (B + lanes - 1) / lanes + 1;
+    auto step_limit = [&](int64_t every) {
+        return windows * ((int64_t)max_iter + 2) + (int64_t)(kLag + 2) * every + 8;
+    };
+    auto drained = [&](unsigned long long occ) { return occ == 0 && !debug_no_drain; };
+    auto overrun = [&](int64_t steps) {
+        set_error("continuous decode of " + std::to_string(B) + " codewords did not drain within " +
+                  std::to_string(steps) + " steps (device lane bookkeeping)");
+        return LDPC_ERR_DEVICE;
+    };
     if (res) {
         // resident pool: every step is check (+ the syndrome of the previous
         // step and the lane bookkeeping, ResStep) then variable (+ the
@@ -897,7 +935,9 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             }
             LDPC_HIP(hipEventRecord(ev_tjoin[0], stream));  // the memsets above
             for (int64_t t = 0; t < tiles; t++) LDPC_HIP(hipStreamWaitEvent(tstream[t], ev_tjoin[0], 0));
+            const int64_t limit = step_limit(every);
             for (int64_t s = 0; rc == LDPC_OK; s++) {
+                if (s >= limit) { rc = overrun(s); break; }
                 const bool poll = (s % every) == every - 1;
                 const int64_t pi = s / every;
                 const int slot = (int)(pi % kRing);
@@ -933,7 +973,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                         LDPC_HIP(hipEventSynchronize(ev_tring[old][t]));
                         occ += h_occ_t[(size_t)old * kMaxTileStreams + t];
                     }
-                    if (occ == 0) break;
+                    if (drained(occ)) break;
                 }
             }
             for (int64_t t = 0; t < tiles; t++) {  // join: later work on `stream` sees every tile's last step
@@ -948,7 +988,9 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             }
             return rc;
         }
+        const int64_t limit = step_limit(every);
         for (int64_t s = 0; rc == LDPC_OK; s++) {
+            if (s >= limit) { rc = overrun(s); break; }
             const bool poll = (s % every) == every - 1;
             const int64_t pi = s / every;
             const int slot = (int)(pi % kRing);
@@ -973,7 +1015,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             if (poll && pi >= kLag) {
                 const int old = (int)((pi - kLag) % kRing);
                 LDPC_HIP(hipEventSynchronize(ev_ring[old]));
-                if (h_occ[old] == 0) break;
+                if (drained(h_occ[old])) break;
             }
         }
         return rc;
@@ -987,7 +1029,9 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         const Refill rfr{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
                          d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
         bool low = false;
+        const int64_t limit = step_limit(1);
         for (int64_t s = 0;; s++) {
+            if (s >= limit) return overrun(s);
             const int slot = (int)(s % kRing);
             rs.cs.occ_count = d_ctr + 1 + slot;
             LDPC_HIP(hipMemsetAsync(rs.cs.occ_count, 0, sizeof(unsigned long long), stream));
@@ -1006,7 +1050,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             if (s >= kLag) {
                 const int old = (int)((s - kLag) % kRing);
                 LDPC_HIP(hipEventSynchronize(ev_ring[old]));
-                if (h_occ[old] == 0) break;
+                if (drained(h_occ[old])) break;
                 low = h_occ[old] * 32 < (unsigned long long)(tiles * 64);
             }
         }
@@ -1025,7 +1069,9 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         LDPC_HIP(hipMemsetAsync(d_unsat, 0, (size_t)tiles * sizeof(unsigned long long), stream));
         LDPC_HIP(hipMemsetAsync(d_done, 0, (size_t)tiles * sizeof(unsigned int), stream));
     }
+    const int64_t limit = step_limit(1);
     for (int64_t s = 0;; s++) {
+        if (s >= limit) return overrun(s);
         const int slot = (int)(s % kRing);
         cs.occ_count = d_ctr + 1 + slot;
         rss.cs.occ_count = cs.occ_count;
@@ -1051,7 +1097,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         if (s >= kLag) {
             const int old = (int)((s - kLag) % kRing);
             LDPC_HIP(hipEventSynchronize(ev_ring[old]));
-            if (h_occ[old] == 0) break;
+            if (drained(h_occ[old])) break;
             low = h_occ[old] * 32 < (unsigned long long)(tiles * 64);
         }
     }

@@ -43,6 +43,7 @@ struct Engine {
     bool lr_csc = false;      // c2v scratch in column (CSC) order (regular kernels only)
     bool cont = false;        // continuous batching: refill lanes as codewords finish
     int full_lanes = 0;       // all lanes of an active tile store (whole cache lines)
+    bool debug_no_drain = false;  // LDPC_DEBUG_NO_DRAIN: the host ignores a drained pool (tests the step bound)
     int var_cpw = 1;          // variable phase: columns per wave (k_var_m when > 1)
     bool msa_c = false;       // min-sum with compressed c2v (records + codes, k_check_msa_c / k_var_msa_c)
     bool res = false;         // resident pool: a few tiles iterated in place (c2v overwrites v2c), syndrome in the check kernel

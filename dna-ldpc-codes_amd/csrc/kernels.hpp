@@ -65,6 +65,24 @@ __device__ __forceinline__ void st(double* p, double v)
     else *p = v;
 }
 
+// Message pointers of the phase kernels: __restrict__ when the input and
+// output messages are distinct buffers; plain pointers when they are the same
+// buffer (the resident pool runs in place: a row's check messages overwrite
+// the variable messages they are computed from, a column's variable messages
+// its check messages).  In place, the order "every load of a row's / column's
+// edges before its first store" is then the source's, which the compiler must
+// keep for possibly aliasing accesses -- it does not rest on the generated ISA.
+template <bool INPLACE>
+struct Msg {
+    using in = const double* __restrict__;
+    using out = double* __restrict__;
+};
+template <>
+struct Msg<true> {
+    using in = const double*;
+    using out = double*;
+};
+
 // The finished codeword's hard bits of the wave's CPW consecutive columns
 // (pre-update ballots), one CPW-byte store per lane when the output is
 // aligned for it (Refill::hard_vec), else byte stores.
@@ -348,8 +366,8 @@ __global__ __launch_bounds__(1024) void k_syndrome(const uint64_t* __restrict__ 
 // ---------------------------------------------------------------------------
 // c2v scratch: CSR order (row-contiguous) or CSC order (column-contiguous,
 // position pos[e]) so the variable phase reads each column contiguously
-template <int DC, bool NT, bool CSCL>
-__device__ __forceinline__ void check_bp_row(const double* __restrict__ src, double* __restrict__ dst,
+template <int DC, bool NT, bool CSCL, bool INPLACE>
+__device__ __forceinline__ void check_bp_row(typename Msg<INPLACE>::in src, typename Msg<INPLACE>::out dst,
                                              const int32_t* __restrict__ prow, int32_t row)
 {
     constexpr int SEG = 8;
@@ -394,8 +412,9 @@ __device__ __forceinline__ void check_bp_row(const double* __restrict__ src, dou
 // SYN (resident pool, ResStep): the lanes run are the tile's occupied ones,
 // every wave also takes its row's parity over the previous variable phase's
 // ballots, and every block ends in res_arrive (no early exit).
-template <int DC, bool NT, bool CSCL, bool SYN>
-__global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ dmsg, double* __restrict__ lr,
+// INPLACE: lr == dmsg (resident pool), see Msg.
+template <int DC, bool NT, bool CSCL, bool SYN, bool INPLACE>
+__global__ __launch_bounds__(256, 2) void k_check_bp(typename Msg<INPLACE>::in dmsg, typename Msg<INPLACE>::out lr,
                                                      const uint64_t* __restrict__ active,
                                                      const int32_t* __restrict__ pos, int32_t M, int64_t E,
                                                      int64_t t0, int full_lanes, ResStep rs)
@@ -423,7 +442,7 @@ __global__ __launch_bounds__(256, 2) void k_check_bp(const double* __restrict__ 
         if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
     }
     if (run)
-        check_bp_row<DC, NT, CSCL>(dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane,
+        check_bp_row<DC, NT, CSCL, INPLACE>(dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane,
                                    lr + (size_t)blockIdx.y * E * TILE + lane, pos + (size_t)row * DC, row);
     if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0);
 }
@@ -535,8 +554,9 @@ __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, d
 // arithmetic of k_var_bp) or min-sum (MSA = true, that of k_var_msa): every
 // c2v load of the wave's columns is issued before the first column's
 // arithmetic -- fewer, longer-lived waves.  Requires N % (4 * CPW) == 0.
-template <bool MSA, int DV, bool NT, bool CONT, int CPW>
-__global__ __launch_bounds__(256) void k_var_m(const double* __restrict__ c2v, double* __restrict__ v2c,
+// INPLACE: v2c == c2v (resident pool), see Msg.
+template <bool MSA, int DV, bool NT, bool CONT, int CPW, bool INPLACE>
+__global__ __launch_bounds__(256) void k_var_m(typename Msg<INPLACE>::in c2v, typename Msg<INPLACE>::out v2c,
                                                double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                const uint64_t* __restrict__ active,
                                                const int32_t* __restrict__ col_edge, double* __restrict__ post,
@@ -731,8 +751,8 @@ __global__ __launch_bounds__(256) void k_var_bp_gen(const double* __restrict__ l
 // (x >= 0 ? +1 : -1) (NaN counts -1).  c2v = (double)sign * mag.
 // dc == 1: mag stays -1 -> 0, sign 1 -> 0.0 (dec.cpp:1427-1430).
 // ---------------------------------------------------------------------------
-template <int DC, bool NT, bool CSCL>
-__device__ __forceinline__ void check_msa_row(const double* __restrict__ src, double* __restrict__ dst,
+template <int DC, bool NT, bool CSCL, bool INPLACE>
+__device__ __forceinline__ void check_msa_row(typename Msg<INPLACE>::in src, typename Msg<INPLACE>::out dst,
                                               const int32_t* __restrict__ prow, int32_t row)
 {
     double x[DC];
@@ -769,8 +789,8 @@ __device__ __forceinline__ void check_msa_row(const double* __restrict__ src, do
     }
 }
 
-template <int DC, bool NT, bool CSCL, bool SYN>
-__global__ __launch_bounds__(256) void k_check_msa(const double* __restrict__ v2c, double* __restrict__ c2v,
+template <int DC, bool NT, bool CSCL, bool SYN, bool INPLACE>
+__global__ __launch_bounds__(256) void k_check_msa(typename Msg<INPLACE>::in v2c, typename Msg<INPLACE>::out c2v,
                                                    const uint64_t* __restrict__ active,
                                                    const int32_t* __restrict__ pos, int32_t M, int64_t E,
                                                    int64_t t0, int full_lanes, ResStep rs)
@@ -798,7 +818,7 @@ __global__ __launch_bounds__(256) void k_check_msa(const double* __restrict__ v2
         if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
     }
     if (run)
-        check_msa_row<DC, NT, CSCL>(v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane,
+        check_msa_row<DC, NT, CSCL, INPLACE>(v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane,
                                     c2v + (size_t)blockIdx.y * E * TILE + lane, pos + (size_t)row * DC, row);
     if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0);
 }

@@ -34,11 +34,21 @@ POST_LLR, POST_RATIO = 0, 1
 IN_LLR, IN_LR = 0, 1
 H2D, D2H, D2D = 0, 1, 2
 
-# reference decoder_type values (DNA_main.cpp:41-53)
-# (ints are the ABI's LDPC_ALGO_* values; 20 = decoder_type MSA is also accepted)
-_ALGOS = {"bp": ALGO_BP, "msa": ALGO_MSA, "min-sum": ALGO_MSA, 20: ALGO_MSA, "qmsa": ALGO_QMSA,
-          "gallager_a": ALGO_GALLAGER_A, "gallager_b1": ALGO_GALLAGER_B1, "gallager_b2": ALGO_GALLAGER_B2,
-          **{k: k for k in range(6)}}
+# Algorithm selection.  Names select the ABI's LDPC_ALGO_* decoders; an int
+# is the reference's decoder_type (enum DECODER_TYPE, DNA_main.cpp:41-53),
+# mapped as LDPC_Decode (DNA_main.cpp:1565-1594) dispatches it and as bin/ldpc
+# does: 0 BP, 1/2/3 Gallager A/B1/B2, 20/21/22 the float min-sum
+# Run_MSA_Decoder_INF (the DNA build never sets g_precision, so the quantized
+# Run_MSA_Decoder is unreachable from a decoder_type; use the name 'qmsa').
+# The ABI codes themselves are reachable only through the names, so a
+# reference caller's decoder_type never silently picks another decoder.
+_NAMES = {"bp": ALGO_BP, "msa": ALGO_MSA, "min-sum": ALGO_MSA, "qmsa": ALGO_QMSA,
+          "gallager_a": ALGO_GALLAGER_A, "gallager_b1": ALGO_GALLAGER_B1, "gallager_b2": ALGO_GALLAGER_B2}
+DECODER_TYPES = {0: ALGO_BP, 1: ALGO_GALLAGER_A, 2: ALGO_GALLAGER_B1, 3: ALGO_GALLAGER_B2,
+                 20: ALGO_MSA, 21: ALGO_MSA, 22: ALGO_MSA}
+# decoder_type written into result file names (DNA_main.cpp:1047-1048) for a named algorithm
+_RESULT_TYPE = {ALGO_BP: 0, ALGO_GALLAGER_A: 1, ALGO_GALLAGER_B1: 2, ALGO_GALLAGER_B2: 3, ALGO_MSA: 20,
+                ALGO_QMSA: 21}
 
 
 class LdpcError(RuntimeError):
@@ -143,12 +153,22 @@ def device_count() -> int:
 
 
 def _algo(a) -> int:
+    """ABI algorithm code of a name or of a reference decoder_type int."""
     if isinstance(a, str):
-        a = a.lower()
-    if a not in _ALGOS:
-        raise ValueError(f"unknown algorithm {a!r} (use 'bp', 'msa', 'qmsa', 'gallager_a', 'gallager_b1', "
-                         "'gallager_b2')")
-    return _ALGOS[a]
+        if a.lower() in _NAMES:
+            return _NAMES[a.lower()]
+    elif isinstance(a, (int, np.integer)) and not isinstance(a, bool) and int(a) in DECODER_TYPES:
+        return DECODER_TYPES[int(a)]
+    raise ValueError(f"unknown algorithm {a!r} (names: 'bp', 'msa', 'qmsa', 'gallager_a', 'gallager_b1', "
+                     "'gallager_b2'; ints: the reference's decoder_type 0, 1, 2, 3, 20, 21, 22)")
+
+
+def _decoder_type(a) -> int:
+    """The reference decoder_type a call runs as (result file names)."""
+    if isinstance(a, (int, np.integer)) and not isinstance(a, bool):
+        _algo(a)
+        return int(a)
+    return _RESULT_TYPE[_algo(a)]
 
 
 class Graph:
@@ -333,8 +353,7 @@ def decode_files(codeword_base: str, soft_base: str, pchk_base: str, max_iter: i
     <pchk>.pchk from `directory`, writes dec_<codeword>.txt and the result file,
     and returns the statistics.  decoder.py can replace its os.system call
     (decoder.py:557-558, 635-636) with this."""
-    a = _algo(algo)
-    decoder_type = 0 if a == ALGO_BP else 20
+    decoder_type = _decoder_type(algo)
     j = lambda p: os.path.join(directory, p)  # noqa: E731
     g = graph(j(pchk_base + ".pchk"))
     N, M = g.N, g.M
@@ -343,7 +362,7 @@ def decode_files(codeword_base: str, soft_base: str, pchk_base: str, max_iter: i
     cw = np.array(_read_tokens(j(codeword_base + ".txt"), N, int), dtype=np.int64)
     llr = np.array(_read_tokens(j(soft_base + ".txt"), N, float), dtype=np.float64)
     raw = int(np.sum(cw != (llr < 0)))  # LDPC_Raw_Error_Check, AWGN soft decision (DNA_main.cpp:1727-1732)
-    hard, _, iters, valid = g.decode(llr, max_iter=max_iter, algo=a, post=None)
+    hard, _, iters, valid = g.decode(llr, max_iter=max_iter, algo=algo, post=None)
     bit_err = int(np.sum(cw != hard))
     with open(j("dec_" + codeword_base + ".txt"), "w") as f:
         f.write("".join(f"{int(b)} " for b in hard))

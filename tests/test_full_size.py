@@ -61,3 +61,33 @@ def test_full_size_properties(gpu, G, og, codewords, algo, p, seed):
         h = np.empty((1, N), np.uint8)
         dh.download(h, offset=int(b) * N)
         assert np.array_equal(h[0], rh[k]) and it[b] == rit[k] and v[b] == bool(rv[k]), int(b)
+
+
+def test_config3_exact_workload(gpu, G, og, codewords):
+    """SURVEY 8(d) config 3 exactly as bench.py times it: 100 000 codewords of
+    BSC p = 0.02 from the device generator with seed 2026, BP, 50 iterations,
+    the engine's default schedule.  Nothing converges at p = 0.02, so every
+    codeword must run all 50 iterations and end invalid; a random sample of
+    64 codewords equals the oracle bit for bit."""
+    L = gpu
+    B, N, max_iter, seed, p = 100_000, G.N, 50, 2026, 0.02
+    eng = L.Engine(G, 0, "bp")
+    cwbuf = L.DeviceBuffer(0, codewords.nbytes)
+    cwbuf.upload(codewords)
+    din = L.DeviceBuffer(0, B * N * 8)
+    eng.gen_bsc(din.at(0), L.IN_LR, 0, B, cwbuf.at(0), 272, seed, p, synth.LLR_UNIT)
+    dh, dit, dv = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
+    eng.decode(din.at(0), L.IN_LR, B, max_iter, dh.at(0), None, L.POST_LLR, dit.at(0), dv.at(0))
+    eng.sync()
+    it = dit.download(np.empty(B, np.int32))
+    v = dv.download(np.empty(B, np.uint8))
+    assert (it == max_iter).all() and not v.any()
+    rng = np.random.default_rng(seed)
+    idx = np.sort(rng.choice(B, 64, replace=False))
+    llr = np.concatenate([synth.bsc_llrs(codewords, int(b), 1, seed=seed, p=p) for b in idx])
+    rh, _, rit, rv = og.decode_batch(llr, max_iter, algo=0, threads=8, want_post=False)
+    assert (rit == max_iter).all() and not rv.any()
+    for k, b in enumerate(idx):
+        h = np.empty((1, N), np.uint8)
+        dh.download(h, offset=int(b) * N)
+        assert np.array_equal(h[0], rh[k]), int(b)

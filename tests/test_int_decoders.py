@@ -93,3 +93,17 @@ def test_int_decoders_irregular_graph(gpu, oracle_mod, tmp_path):
         h, post, it, v = G.decode(llr, max_iter=25, algo=name, post="llr", **kw)
         rh, rpost, rit, rv = og.decode_int_batch(llr, 25, a, precision=5, step=0.75, beta=1, seed=7, threads=4)
         assert np.array_equal(h, rh) and np.array_equal(it, rit) and np.array_equal(post, rpost), name
+
+
+@pytest.mark.gpu
+def test_reference_decoder_type_ints(gpu, G, codewords):
+    """algo as an int is the reference's decoder_type (DNA_main.cpp:41-53):
+    1 runs Gallager A like 'gallager_a' and bin/ldpc's decoder_type 1, 20/21/22
+    the float min-sum, 0 BP."""
+    llr = synth.bsc_llrs(codewords, 0, 64, seed=5, p=0.004)
+    for t, name in ((1, "gallager_a"), (2, "gallager_b1"), (3, "gallager_b2"), (20, "msa"), (21, "msa"), (0, "bp")):
+        a = G.decode(llr, max_iter=20, algo=t, post=None)
+        b = G.decode(llr, max_iter=20, algo=name, post=None)
+        for x, y in zip(a, b):
+            if x is not None:
+                assert np.array_equal(np.asarray(x), np.asarray(y)), (t, name)

@@ -1,0 +1,104 @@
+"""Sharded decodes on the GPU (BASELINE config 4's path).
+
+* bench.py under torch.distributed.run with 2 ranks (both on the box's one
+  GPU) and --global-batch: each rank decodes its dist.shard of the global
+  range (DNA_main.cpp:629-651 Set_FrameNum's split), and the outputs it
+  dumps equal one single-process decode of the same global range, row for
+  row;
+* ldpc_decode's in-process multi-device path (opts.n_devices, one host
+  thread + stream per device): every visible device, and ragged shards over
+  repeated device ids, bit-exact against the oracle.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import synth
+from test_gpu_parity import _cmp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _line(stdout):
+    lines = [ln for ln in stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def _load(d, world, N):
+    parts = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(world)]
+    parts.sort(key=lambda z: int(z["b0"]))
+    return parts
+
+
+@pytest.mark.timeout(240)
+def test_two_rank_bench_shards_match_single_process(gpu, G, tmp_path):
+    total, args = 1000, ["--global-batch", "1000", "--max-iter", "20", "--p", "0.005", "--steps", "1",
+                         "--warmup", "0", "--no-profile", "--cpu-baseline", "0"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    d2, d1 = str(tmp_path / "two"), str(tmp_path / "one")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dump-dir", d2, *args],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out2 = _line(r.stdout)
+    assert out2["n_gpus"] == 2 and out2["scaling"] == "strong"
+    assert out2["config"]["per_rank"] == [500, 500] and out2["config"]["global_batch"] == total
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dump-dir", d1, *args], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out1 = _line(r.stdout)
+    assert out1["n_gpus"] == 1 and out1["config"]["per_rank"] == [total]
+    two = _load(d2, 2, G.N)
+    one = _load(d1, 1, G.N)[0]
+    assert [int(z["b0"]) for z in two] == [0, 500] and [int(z["B"]) for z in two] == [500, 500]
+    for z in two:
+        b0, B = int(z["b0"]), int(z["B"])
+        assert np.array_equal(z["iters"], one["iters"][b0:b0 + B])
+        assert np.array_equal(z["valid"], one["valid"][b0:b0 + B])
+        assert np.array_equal(z["hard"], one["hard"][b0:b0 + B])
+    it = one["iters"]
+    assert len(np.unique(it)) > 2 and one["valid"].any() and not one["valid"].all()
+
+
+def test_bench_global_batch_odd_split(gpu, tmp_path):
+    """A global batch that does not divide: dist.shard sizes differ by one;
+    single process -> the whole range."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--global-batch", "129", "--max-iter", "5",
+                        "--steps", "1", "--warmup", "0", "--cpu-seconds", "0.5", "--dump-dir", str(tmp_path)],
+                       cwd=ROOT, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = _line(r.stdout)
+    assert out["config"]["per_rank"] == [129] and out["scaling"] == "strong"
+    assert out["check"]["mismatches"] == 0 and out["check"]["checked"] >= 16
+    z = np.load(os.path.join(tmp_path, "rank0.npz"))
+    assert int(z["B"]) == 129 and z["iters"].shape == (129,)
+
+
+def test_ldpc_decode_every_visible_device(gpu, G, og, codewords):
+    """opts.n_devices = device_count(): the in-process multi-GPU path on
+    every device of the box (one on a one-GPU box, eight on a node)."""
+    n = gpu.device_count()
+    llr = synth.bsc_llrs(codewords, 0, 64 * n + 37, seed=12, p=0.005)
+    _cmp(G, og, llr, 25, devices=list(range(n)))
+
+
+@pytest.mark.parametrize("devs,B", [([0, 0, 0], 200), ([0, 0, 0, 0, 0], 7), ([0, 0], 1)])
+def test_ldpc_decode_ragged_shards(G, og, codewords, devs, B):
+    """Ragged shards: B not divisible by the device count, shards smaller than
+    a tile, more devices than codewords (empty shards)."""
+    llr = synth.bsc_llrs(codewords, 3, B, seed=13, p=0.005)
+    _cmp(G, og, llr, 25, devices=devs)

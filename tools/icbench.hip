@@ -88,12 +88,12 @@ int main(int argc, char** argv)
     const dim3 blk(256);
     const Refill rf{};
     auto check = [&](const double* src, double* dst, int64_t t0, unsigned gt, bool nt) {
-        if (nt) hipLaunchKernelGGL((k_check_bp<72, true, false, false>), dim3(M / 4, gt), blk, 0, 0, src, dst, active, d_pos, M, E, t0, 1, ResStep{});
-        else hipLaunchKernelGGL((k_check_bp<72, false, false, false>), dim3(M / 4, gt), blk, 0, 0, src, dst, active, d_pos, M, E, t0, 1, ResStep{});
+        if (nt) hipLaunchKernelGGL((k_check_bp<72, true, false, false, false>), dim3(M / 4, gt), blk, 0, 0, src, dst, active, d_pos, M, E, t0, 1, ResStep{});
+        else hipLaunchKernelGGL((k_check_bp<72, false, false, false, false>), dim3(M / 4, gt), blk, 0, 0, src, dst, active, d_pos, M, E, t0, 1, ResStep{});
     };
     auto var = [&](const double* src, double* dst, int64_t t0, unsigned gt, bool nt) {
-        if (nt) hipLaunchKernelGGL((k_var_m<false, 8, true, false, 4>), dim3(N / 16, gt), blk, 0, 0, src, dst, prior, hard, active, d_col_edge, (double*)nullptr, N, E, t0, rf, 1);
-        else hipLaunchKernelGGL((k_var_m<false, 8, false, false, 4>), dim3(N / 16, gt), blk, 0, 0, src, dst, prior, hard, active, d_col_edge, (double*)nullptr, N, E, t0, rf, 1);
+        if (nt) hipLaunchKernelGGL((k_var_m<false, 8, true, false, 4, false>), dim3(N / 16, gt), blk, 0, 0, src, dst, prior, hard, active, d_col_edge, (double*)nullptr, N, E, t0, rf, 1);
+        else hipLaunchKernelGGL((k_var_m<false, 8, false, false, 4, false>), dim3(N / 16, gt), blk, 0, 0, src, dst, prior, hard, active, d_col_edge, (double*)nullptr, N, E, t0, rf, 1);
     };
     const double algo_bytes = (32.0 * E + 10.0 * N) * 64;  // per tile-iteration
     auto report = [&](const char* name, float ms, double tile_iters) {
@@ -168,8 +168,8 @@ int main(int argc, char** argv)
         for (int G : {3, 4}) {
             float ms = timeit([&] {
                 for (int t0 = 0; t0 + G <= P; t0 += G) {
-                    hipLaunchKernelGGL((k_check_msa<72, true, false, false>), dim3(M / 4, G), blk, 0, 0, d, scr, active, d_pos, M, E, (int64_t)t0, 1, ResStep{});
-                    hipLaunchKernelGGL((k_var_m<true, 8, true, false, 4>), dim3(N / 16, G), blk, 0, 0, scr, d, prior, hard, active, d_col_edge, (double*)nullptr, N, E, (int64_t)t0, rf, 1);
+                    hipLaunchKernelGGL((k_check_msa<72, true, false, false, false>), dim3(M / 4, G), blk, 0, 0, d, scr, active, d_pos, M, E, (int64_t)t0, 1, ResStep{});
+                    hipLaunchKernelGGL((k_var_m<true, 8, true, false, 4, false>), dim3(N / 16, G), blk, 0, 0, scr, d, prior, hard, active, d_col_edge, (double*)nullptr, N, E, (int64_t)t0, rf, 1);
                 }
             });
             char nm[64];
