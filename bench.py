@@ -295,6 +295,11 @@ def main():
             # variable phase: read E lr + N LR, write E d + N/8 hard-bit ballots
             "variable": 16.0 * E + 8.0 * N + N / 8.0,
         }
+    if eng.pingpong:
+        # ping-pong schedule: every launch is one tile's check phase plus
+        # another tile's variable phase (k_pingpong_bp, counted as "check")
+        by_kernel["check"] = by_kernel["check"] + by_kernel["variable"]
+
     def avg_ms(k):
         return st[k]["ms"] / st[k]["sampled"] if st[k]["sampled"] else 0.0
 
@@ -308,6 +313,8 @@ def main():
     # traffic: HBM bytes per codeword-iteration of this kernel from the committed
     # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE), scaled to this launch size
     kname = f"k_{'check' if dom == 'check' else 'var'}_{algo}" + ("_c" if eng.msa_compressed else "")
+    if eng.pingpong:
+        kname = "k_pingpong_bp"
     traffic, traffic_src = None, None
     for tf in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
         tj = json.load(open(tf))
@@ -364,6 +371,7 @@ def main():
                    "resident_per_pass": eng.cap, "group_tiles": eng.group_tiles, "nontemporal_d": eng.nontemporal,
                    "two_stream": eng.pipeline, "continuous": eng.continuous, "resident_pool": eng.resident,
                    "compressed_msa": eng.msa_compressed, "syndrome_split": eng.syndrome_split,
+                   "pingpong": eng.pingpong,
                    "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 4)},
         "roofline": roof,
     }

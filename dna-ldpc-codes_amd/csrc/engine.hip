@@ -52,6 +52,8 @@ constexpr int64_t kDefaultSynSplit = 32;     // LDPC_SYN_SPLIT: syndrome blocks 
 constexpr int64_t kDefaultSynFused = 0;      // LDPC_SYN_FUSED: grouped continuous mode, syndrome fused into the check kernel
 constexpr int64_t kDefaultResMsaC = 0;       // LDPC_RES_MSA_C: resident pool for compressed min-sum
 constexpr int64_t kDefaultResTilesMsaC = 2;  // LDPC_RES_TILES_MSA_C: its pool tiles   // LDPC_RES_POLL: steps between occupancy polls
+constexpr int64_t kDefaultPingpong = 0;      // LDPC_PINGPONG: resident BP pool, check(t) + variable(t-1) per launch
+constexpr int64_t kDefaultPpCpw = 4;         // LDPC_PP_CPW: its variable-phase columns per wave
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
@@ -154,6 +156,10 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         csc = 0;
         res_poll = (int)std::max<int64_t>(1, env_int("LDPC_RES_POLL", kDefaultResPoll));
         res_syn_split = (int)std::max<int64_t>(0, std::min<int64_t>(env_int("LDPC_RES_SYN", kDefaultResSyn), 256));
+        pp_cpw = (int)env_int("LDPC_PP_CPW", kDefaultPpCpw);
+        pingpong = !msa_c && algo == LDPC_ALGO_BP && res_syn_split == 0 && !tile_streams &&
+                   env_int("LDPC_PINGPONG", kDefaultPingpong) != 0 && (pp_cpw == 2 || pp_cpw == 4 || pp_cpw == 8) &&
+                   g->N % (4 * pp_cpw) == 0;
     }
     if (chunk <= 0) {
         size_t fr = 0, tot = 0;
@@ -636,6 +642,31 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
     return LDPC_OK;
 }
 
+// resident BP pool, ping-pong schedule: check(tc) + variable(tv) in one launch
+// (kernels.hpp k_pingpong_bp); tv < 0: check only
+int Engine::launch_pingpong(hipStream_t s, int64_t tc, int64_t tv, double* pt, const dev::ResStep& rs,
+                            const dev::Refill& rf)
+{
+    using namespace dev;
+    const int32_t M = g->M, N = g->N;
+    const int64_t E = g->E;
+    const uint32_t nchk = (uint32_t)((M + 3) / 4);
+    const uint32_t nvar = tv < 0 ? 0u : (uint32_t)(N / (4 * pp_cpw));
+    const dim3 grid(nchk + nvar), blk(256);
+    LAUNCH_ON(s, K_CHECK, {
+        if (pp_cpw == 2)
+            hipLaunchKernelGGL((k_pingpong_bp<72, 8, 2>), grid, blk, 0, s, v2c, prior, hard, active, d_col_edge, pt, M,
+                               N, E, tc, tv, nchk, nvar, full_lanes, rs, rf);
+        else if (pp_cpw == 8)
+            hipLaunchKernelGGL((k_pingpong_bp<72, 8, 8>), grid, blk, 0, s, v2c, prior, hard, active, d_col_edge, pt, M,
+                               N, E, tc, tv, nchk, nvar, full_lanes, rs, rf);
+        else
+            hipLaunchKernelGGL((k_pingpong_bp<72, 8, 4>), grid, blk, 0, s, v2c, prior, hard, active, d_col_edge, pt, M,
+                               N, E, tc, tv, nchk, nvar, full_lanes, rs, rf);
+    });
+    return LDPC_OK;
+}
+
 // variable phase (+ hard decisions, optional posterior) of tiles t0 .. t0+gt-1
 int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt, const dev::Refill& rf)
 {
@@ -923,6 +954,37 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         // host stops at most kLag steps after the pool empties
         const int every = B <= 8 * cap ? 1 : res_poll;
         int rc = LDPC_OK;
+        if (pingpong && tiles >= 2) {
+            // ping-pong: step s = launches (s, t) for t = 0..tiles-1, each the
+            // check of tile t and the variable phase of tile t-1 (mod tiles),
+            // checked by the launch before.  The poll counter spans one whole
+            // step (every tile's bookkeeping).  The decode stops kLag polls
+            // after the pool drained, so the last tile's variable phase left
+            // pending by the final step has no finished lane to write.
+            const int64_t limit = step_limit(every);
+            for (int64_t s = 0; rc == LDPC_OK; s++) {
+                if (s >= limit) { rc = overrun(s); break; }
+                const bool poll = (s % every) == every - 1;
+                const int64_t pi = s / every;
+                const int slot = (int)(pi % kRing);
+                rs.cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
+                if (poll) LDPC_HIP(hipMemsetAsync(rs.cs.occ_count, 0, sizeof(unsigned long long), stream));
+                for (int64_t t = 0; t < tiles && rc == LDPC_OK; t++)
+                    rc = launch_pingpong(stream, t, (s == 0 && t == 0) ? -1 : (t + tiles - 1) % tiles, pt, rs, rfr);
+                if (rc) break;
+                if (poll) {
+                    LDPC_HIP(hipMemcpyAsync(h_occ + slot, rs.cs.occ_count, sizeof(unsigned long long),
+                                            hipMemcpyDeviceToHost, stream));
+                    LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
+                }
+                if (poll && pi >= kLag) {
+                    const int old = (int)((pi - kLag) % kRing);
+                    LDPC_HIP(hipEventSynchronize(ev_ring[old]));
+                    if (drained(h_occ[old])) break;
+                }
+            }
+            return rc;
+        }
         if (tile_streams && !msa_c && res_syn_split == 0 && tiles <= kMaxTileStreams) {
             // one stream per pool tile: the tiles' check/variable chains are
             // independent (lane bookkeeping, refill claims and occupancy are

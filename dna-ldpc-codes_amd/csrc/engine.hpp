@@ -44,6 +44,8 @@ struct Engine {
     bool cont = false;        // continuous batching: refill lanes as codewords finish
     int full_lanes = 0;       // all lanes of an active tile store (whole cache lines)
     bool debug_no_drain = false;  // LDPC_DEBUG_NO_DRAIN: the host ignores a drained pool (tests the step bound)
+    bool pingpong = false;    // res, BP: one launch = check(tile t) + variable(tile t-1), k_pingpong_bp (LDPC_PINGPONG)
+    int pp_cpw = 4;           // pingpong: variable-phase columns per wave (LDPC_PP_CPW)
     int var_cpw = 1;          // variable phase: columns per wave (k_var_m when > 1)
     bool msa_c = false;       // min-sum with compressed c2v (records + codes, k_check_msa_c / k_var_msa_c)
     bool res = false;         // resident pool: a few tiles iterated in place (c2v overwrites v2c), syndrome in the check kernel
@@ -137,6 +139,8 @@ struct Engine {
     int probe_res(int probes);
     int launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt);
     int launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt, const dev::Refill& rf);
+    int launch_pingpong(hipStream_t s, int64_t tc, int64_t tv, double* pt, const dev::ResStep& rs,
+                        const dev::Refill& rf);
 };
 
 // bytes of device memory per resident codeword

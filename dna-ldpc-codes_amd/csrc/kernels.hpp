@@ -204,12 +204,12 @@ __device__ __forceinline__ uint64_t row_parity(const uint64_t* __restrict__ h, c
 }
 
 // Resident pool epilogue of a check block (all 256 threads): OR the block's
-// row parities into unsat[t]; the last block of the tile to arrive runs the
+// row parities into unsat[t]; the last of the tile's nblk blocks to arrive runs the
 // lane bookkeeping for the step (cont_lanes: iters / valid, refill claims,
 // active / fresh / occupied masks) and hands the finished lanes to the
 // variable kernel, which writes their outputs before refilling them.
 __device__ __forceinline__ void res_arrive(int64_t t, uint64_t occ, uint64_t p, const ResStep& rs, int32_t ln0,
-                                           int64_t b0)
+                                           int64_t b0, uint32_t nblk)
 {
     __shared__ uint64_t red[4];
     __shared__ int64_t s_b[TILE];
@@ -229,7 +229,7 @@ __device__ __forceinline__ void res_arrive(int64_t t, uint64_t occ, uint64_t p, 
         unsigned long long o = 0;
         if (U) o = atomicOr(rs.unsat + t, (unsigned long long)U);
         asm volatile("" ::"v"(o) : "memory");
-        s_last = atomicAdd(rs.done + t, 1u) == gridDim.x - 1;
+        s_last = atomicAdd(rs.done + t, 1u) == nblk - 1;
     }
     __syncthreads();
     if (!s_last) return;
@@ -413,15 +413,15 @@ __device__ __forceinline__ void check_bp_row(typename Msg<INPLACE>::in src, type
 // every wave also takes its row's parity over the previous variable phase's
 // ballots, and every block ends in res_arrive (no early exit).
 // INPLACE: lr == dmsg (resident pool), see Msg.
+// Block rb of nrb row blocks of tile t; lr_t = the tile's c2v messages.
 template <int DC, bool NT, bool CSCL, bool SYN, bool INPLACE>
-__global__ __launch_bounds__(256, 2) void k_check_bp(typename Msg<INPLACE>::in dmsg, typename Msg<INPLACE>::out lr,
-                                                     const uint64_t* __restrict__ active,
-                                                     const int32_t* __restrict__ pos, int32_t M, int64_t E,
-                                                     int64_t t0, int full_lanes, ResStep rs)
+__device__ __forceinline__ void check_bp_block(typename Msg<INPLACE>::in dmsg, typename Msg<INPLACE>::out lr_t,
+                                               const uint64_t* __restrict__ active, const int32_t* __restrict__ pos,
+                                               int32_t M, int64_t E, int64_t t, uint32_t rb, uint32_t nrb,
+                                               int full_lanes, const ResStep& rs)
 {
     const int lane = lane_id();
-    const int32_t row = blockIdx.x * 4 + wave_id();
-    const int64_t t = t0 + blockIdx.y;
+    const int32_t row = (int32_t)rb * 4 + wave_id();
     const uint64_t act = SYN ? rs.cs.occupied[t] : active[t];
     // full_lanes: converged / empty lanes of an active tile run along on their
     // stale state so every c2v store covers whole lines (their values are never read)
@@ -442,9 +442,19 @@ __global__ __launch_bounds__(256, 2) void k_check_bp(typename Msg<INPLACE>::in d
         if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
     }
     if (run)
-        check_bp_row<DC, NT, CSCL, INPLACE>(dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane,
-                                   lr + (size_t)blockIdx.y * E * TILE + lane, pos + (size_t)row * DC, row);
-    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0);
+        check_bp_row<DC, NT, CSCL, INPLACE>(dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane, lr_t + lane,
+                                            pos + (size_t)row * DC, row);
+    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0, nrb);
+}
+
+template <int DC, bool NT, bool CSCL, bool SYN, bool INPLACE>
+__global__ __launch_bounds__(256, 2) void k_check_bp(typename Msg<INPLACE>::in dmsg, typename Msg<INPLACE>::out lr,
+                                                     const uint64_t* __restrict__ active,
+                                                     const int32_t* __restrict__ pos, int32_t M, int64_t E,
+                                                     int64_t t0, int full_lanes, ResStep rs)
+{
+    check_bp_block<DC, NT, CSCL, SYN, INPLACE>(dmsg, lr + (size_t)blockIdx.y * E * TILE, active, pos, M, E,
+                                               t0 + blockIdx.y, blockIdx.x, gridDim.x, full_lanes, rs);
 }
 
 // Generic row degree: the prefix products go through the lr array exactly as
@@ -555,16 +565,16 @@ __global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, d
 // c2v load of the wave's columns is issued before the first column's
 // arithmetic -- fewer, longer-lived waves.  Requires N % (4 * CPW) == 0.
 // INPLACE: v2c == c2v (resident pool), see Msg.
+// Column block cb (4 waves x CPW columns) of tile t; c2v_t = the tile's c2v messages.
 template <bool MSA, int DV, bool NT, bool CONT, int CPW, bool INPLACE>
-__global__ __launch_bounds__(256) void k_var_m(typename Msg<INPLACE>::in c2v, typename Msg<INPLACE>::out v2c,
-                                               double* __restrict__ prior, uint64_t* __restrict__ hard,
-                                               const uint64_t* __restrict__ active,
-                                               const int32_t* __restrict__ col_edge, double* __restrict__ post,
-                                               int32_t N, int64_t E, int64_t t0, Refill rf, int full_lanes)
+__device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typename Msg<INPLACE>::out v2c,
+                                            double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                            const uint64_t* __restrict__ active, const int32_t* __restrict__ col_edge,
+                                            double* __restrict__ post, int32_t N, int64_t E, int64_t t, uint32_t cb,
+                                            const Refill& rf, int full_lanes)
 {
     const int lane = lane_id();
-    const int32_t j0 = (xcd_block(blockIdx.x, gridDim.x) * 4 + wave_id()) * CPW;
-    const int64_t t = t0 + blockIdx.y;
+    const int32_t j0 = ((int32_t)cb * 4 + wave_id()) * CPW;
     if (j0 >= N) return;
     const uint64_t act = active[t];
     const uint64_t frm = CONT ? rf.fresh[t] : 0ull;
@@ -582,7 +592,7 @@ __global__ __launch_bounds__(256) void k_var_m(typename Msg<INPLACE>::in c2v, ty
         fb = rf.fin_b[t * TILE + lane];
         fn = rf.fin_n[t * TILE + lane];
     }
-    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
+    const size_t tb = (size_t)t * E;
     int32_t eid[CPW][DV];
 #pragma unroll
     for (int c = 0; c < CPW; ++c)
@@ -601,7 +611,7 @@ __global__ __launch_bounds__(256) void k_var_m(typename Msg<INPLACE>::in c2v, ty
             pv[c] = (full_lanes & 2) ? ld<true>(prior + ((size_t)t * N + j0 + c) * TILE + lane)
                                      : prior[((size_t)t * N + j0 + c) * TILE + lane];
 #pragma unroll
-            for (int s = 0; s < DV; ++s) l[c][s] = c2v[(tl + (size_t)eid[c][s]) * TILE + lane];
+            for (int s = 0; s < DV; ++s) l[c][s] = c2v_t[(size_t)eid[c][s] * TILE + lane];
         }
     }
     if (CONT && fl) {  // finished codeword: hard bits of its exit (ballots before this step's update)
@@ -691,6 +701,53 @@ __global__ __launch_bounds__(256) void k_var_m(typename Msg<INPLACE>::in c2v, ty
             hard[o] = (old & ~touched) | (m & touched);
         }
     }
+}
+
+template <bool MSA, int DV, bool NT, bool CONT, int CPW, bool INPLACE>
+__global__ __launch_bounds__(256) void k_var_m(typename Msg<INPLACE>::in c2v, typename Msg<INPLACE>::out v2c,
+                                               double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                               const uint64_t* __restrict__ active,
+                                               const int32_t* __restrict__ col_edge, double* __restrict__ post,
+                                               int32_t N, int64_t E, int64_t t0, Refill rf, int full_lanes)
+{
+    var_m_block<MSA, DV, NT, CONT, CPW, INPLACE>(c2v + (size_t)blockIdx.y * E * TILE, v2c, prior, hard, active,
+                                                 col_edge, post, N, E, t0 + blockIdx.y,
+                                                 xcd_block(blockIdx.x, gridDim.x), rf, full_lanes);
+}
+
+// Resident pool, ping-pong schedule (engine `pingpong`, BP): ONE launch runs
+// the check phase of pool tile tc (+ its syndrome and lane bookkeeping, as
+// k_check_bp<SYN>) and the variable phase of tile tv, the tile the previous
+// launch checked (+ its finished lanes' outputs and refills, as k_var_m).
+// Blocks of the two kinds are interleaved in dispatch order (nchk check
+// blocks spread evenly over the nchk + nvar blocks of the grid, after the
+// XCD-affine renumbering), so the chip runs both access shapes at once -- the
+// contiguous 72-edge rows beside the scattered 8-edge columns -- instead of
+// whole-pool launches of one shape.  Each tile's phases still alternate check,
+// variable, check, ... in launch order (tv was checked by the previous launch,
+// tc's last variable phase ran P - 1 launches ago, P = pool tiles >= 2), so
+// every codeword's arithmetic is that of k_check_bp / k_var_m.  In place:
+// msg holds the pool's messages (d between the phases, lr inside a step).
+// tv < 0 (the first launch of a decode): nvar == 0.
+template <int DC, int DV, int CPW>
+__global__ __launch_bounds__(256, 2) void k_pingpong_bp(double* msg, double* __restrict__ prior,
+                                                        uint64_t* __restrict__ hard, const uint64_t* __restrict__ active,
+                                                        const int32_t* __restrict__ col_edge,
+                                                        double* __restrict__ post, int32_t M, int32_t N, int64_t E,
+                                                        int64_t tc, int64_t tv, uint32_t nchk, uint32_t nvar,
+                                                        int full_lanes, ResStep rs, Refill rf)
+{
+    const uint32_t T = nchk + nvar;
+    const uint32_t L = xcd_block(blockIdx.x, T);
+    // check blocks before logical block L: floor(L * nchk / T)
+    const uint32_t c0 = (uint32_t)(((uint64_t)L * nchk) / T);
+    const uint32_t c1 = (uint32_t)(((uint64_t)(L + 1) * nchk) / T);
+    if (c1 > c0)
+        check_bp_block<DC, false, false, true, true>(msg, msg + (size_t)tc * E * TILE, active, nullptr, M, E, tc, c0,
+                                                     nchk, full_lanes, rs);
+    else
+        var_m_block<false, DV, false, true, CPW, true>(msg + (size_t)tv * E * TILE, msg, prior, hard, active,
+                                                       col_edge, post, N, E, tv, L - c0, rf, full_lanes);
 }
 
 // Generic column degree: the partial products go through the v2c array
@@ -820,7 +877,7 @@ __global__ __launch_bounds__(256) void k_check_msa(typename Msg<INPLACE>::in v2c
     if (run)
         check_msa_row<DC, NT, CSCL, INPLACE>(v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane,
                                     c2v + (size_t)blockIdx.y * E * TILE + lane, pos + (size_t)row * DC, row);
-    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0);
+    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0, gridDim.x);
 }
 
 __global__ __launch_bounds__(256) void k_check_msa_gen(const double* __restrict__ v2c, double* __restrict__ c2v,
@@ -1056,7 +1113,7 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
         if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
     }
     if (run) check_msa_c_row<DC, NT>(v2c, codes, rec, M, E, t, row);
-    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0);
+    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0, gridDim.x);
 }
 
 // Min-sum variable phase on compressed messages (arithmetic of k_var_m<MSA>).
@@ -1358,7 +1415,7 @@ __global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs)
         u |= shfl_xor_u64(u, 2);
         u |= shfl_xor_u64(u, 4);
     }
-    res_arrive(t, occ, u, rs, ln0, b0);
+    res_arrive(t, occ, u, rs, ln0, b0, gridDim.x);
 }
 
 // hard ballots -> [b][N] u8 (the reference's dblk / dec_*.txt bits)

@@ -452,6 +452,7 @@ class Engine:
         self.syndrome_split = bool(fl.value & 64)  # multi-block continuous-mode syndrome (LDPC_SYN_SPLIT)
         self.syndrome_fused = bool(fl.value & 128)  # syndrome in the grouped check launches (LDPC_SYN_FUSED)
         self.tile_streams = bool(fl.value & 256)  # resident pool, one stream per tile (LDPC_RES_STREAMS)
+        self.pingpong = bool(fl.value & 512)  # resident BP pool, check(t) + variable(t-1) per launch (LDPC_PINGPONG)
 
     def decode(self, d_in, in_kind: int, B: int, max_iter: int, d_hard=None, d_post=None, post_kind=POST_LLR,
                d_iters=None, d_valid=None):

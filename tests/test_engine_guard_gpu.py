@@ -16,7 +16,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.timeout(120)
 @pytest.mark.parametrize("algo,env", [("bp", {}), ("bp", {"LDPC_RES": "0"}), ("msa", {}),
-                                      ("bp", {"LDPC_RES_STREAMS": "1"}), ("msa", {"LDPC_MSA_C": "0"})])
+                                      ("bp", {"LDPC_RES_STREAMS": "1"}), ("msa", {"LDPC_MSA_C": "0"}),
+                                      ("bp", {"LDPC_PINGPONG": "1"})])
 def test_undrained_decode_is_bounded(gpu, og, codewords, monkeypatch, algo, env):
     L = gpu
     monkeypatch.setenv("LDPC_DEBUG_NO_DRAIN", "1")

@@ -527,3 +527,41 @@ def test_resident_pool_tile_streams_bitexact(gpu, og, codewords, monkeypatch, al
     assert len(np.unique(it)) > 2
     _cmp(G2, og, llr[:70], 0, algo=algo, chunk=64 * tiles)
     _cmp(G2, og, llr[:3], 20, algo=algo, chunk=64 * tiles)
+
+
+@pytest.mark.parametrize("tiles,cpw,poll", [(2, 4, 4), (3, 4, 1), (3, 2, 3), (4, 8, 2), (2, 8, 1)])
+def test_pingpong_bitexact(gpu, og, codewords, monkeypatch, tiles, cpw, poll):
+    """Ping-pong schedule of the resident BP pool (kernels.hpp k_pingpong_bp:
+    one launch = check(tile t) + variable(tile t-1)): only the launch grouping
+    across codewords changes, never a codeword's arithmetic -- mixed early
+    exits, all lanes at max_iter, max_iter 0, batches smaller than the pool,
+    posterior ratio, NaN / inf inputs."""
+    monkeypatch.setenv("LDPC_PINGPONG", "1")
+    monkeypatch.setenv("LDPC_RES", "1")
+    monkeypatch.setenv("LDPC_RES_TILES", str(tiles))
+    monkeypatch.setenv("LDPC_RES_POLL", str(poll))
+    monkeypatch.setenv("LDPC_PP_CPW", str(cpw))
+    G2 = gpu.Graph(PCHK)
+    e = gpu.Engine(G2, 0, "bp", chunk=64 * tiles)
+    assert e.pingpong and e.resident
+    del e
+    llr = synth.dna_like_llrs(codewords, seed=1, reads=57000)[:200]
+    _cmp(G2, og, llr, 60, chunk=64 * tiles)
+    llr = np.concatenate([synth.bsc_llrs(codewords, 0, 150, seed=3, p=0.003),
+                          synth.bsc_llrs(codewords, 150, 130, seed=2026, p=0.02)])
+    _, _, it, _ = _cmp(G2, og, llr, 50, chunk=64 * tiles)
+    assert (it[150:] == 50).all() and len(np.unique(it[:150])) > 2
+    _cmp(G2, og, llr[:70], 0, chunk=64 * tiles)
+    _cmp(G2, og, llr[:5], 50, chunk=64 * tiles)
+    _cmp(G2, og, llr[:130], 7, chunk=64 * tiles)
+    rng = np.random.default_rng(21)
+    llr = synth.dna_like_llrs(codewords, seed=2, reads=60000)[:100]
+    llr[rng.random(llr.shape) < 0.002] = np.nan
+    llr[rng.random(llr.shape) < 0.002] = np.inf
+    llr[rng.random(llr.shape) < 0.002] = -np.inf
+    ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 40, algo=0, post_mode=1, threads=8)
+    h, p, it, v = G2.decode(llr, max_iter=40, algo="bp", post="ratio", chunk=64 * tiles)
+    assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
+    nan = np.isnan(ref_p)
+    assert np.array_equal(np.isnan(p), nan)
+    assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64))
