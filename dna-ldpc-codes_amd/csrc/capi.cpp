@@ -261,6 +261,18 @@ int ldpc_graph_info(const ldpc_graph* g, int32_t* M, int32_t* N, int64_t* E, int
     return LDPC_OK;
 }
 
+int ldpc_graph_blocks(const ldpc_graph* g, int32_t* Q, int32_t* row_blocks, int32_t* col_blocks, int32_t* col_block)
+{
+    if (!g) { set_error("null graph"); return LDPC_ERR_ARG; }
+    const ldpc::XrLayout* L = ldpc::xr_layout_of(g->h);
+    if (Q) *Q = L ? L->Q : 0;
+    if (row_blocks) *row_blocks = L ? L->GA : 0;
+    if (col_blocks) *col_blocks = L ? L->RB : 0;
+    if (L && col_block)
+        for (size_t q = 0; q < L->col_orig.size(); q++) col_block[L->col_orig[q]] = (int32_t)(q / (size_t)L->Q);
+    return LDPC_OK;
+}
+
 int ldpc_graph_edges(const ldpc_graph* g, int32_t* row_ptr, int32_t* col_idx, int32_t* col_ptr, int32_t* col_edge)
 {
     if (!g) { set_error("null graph"); return LDPC_ERR_ARG; }
@@ -463,7 +475,7 @@ int ldpc_engine_info(ldpc_engine* e, int64_t* cap, int64_t* group_tiles, int32_t
     if (flags) *flags = (e->e->nt_d ? 1 : 0) | (e->e->pipe ? 2 : 0) | (e->e->lr_csc ? 4 : 0) | (e->e->cont ? 8 : 0) |
                         (e->e->msa_c ? 16 : 0) | (e->e->res ? 32 : 0) | (e->e->syn_split ? 64 : 0) |
                         (e->e->syn_fused ? 128 : 0) | (e->e->res && e->e->tile_streams ? 256 : 0) |
-                        (e->e->res && e->e->pingpong ? 512 : 0);
+                        (e->e->res && e->e->pingpong ? 512 : 0) | (e->e->xr ? 1024 : 0);
     return LDPC_OK;
 }
 

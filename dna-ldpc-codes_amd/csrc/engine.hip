@@ -21,11 +21,13 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 
 #include "engine.hpp"
 #include "kernels.hpp"
 #include "kernels_int.hpp"
+#include "kernels_xr.hpp"
 
 #include <cstdlib>
 
@@ -54,6 +56,10 @@ constexpr int64_t kDefaultResMsaC = 0;       // LDPC_RES_MSA_C: resident pool fo
 constexpr int64_t kDefaultResTilesMsaC = 2;  // LDPC_RES_TILES_MSA_C: its pool tiles   // LDPC_RES_POLL: steps between occupancy polls
 constexpr int64_t kDefaultPingpong = 0;      // LDPC_PINGPONG: resident BP pool, check(t) + variable(t-1) per launch
 constexpr int64_t kDefaultPpCpw = 4;         // LDPC_PP_CPW: its variable-phase columns per wave
+constexpr int64_t kDefaultXr = 0;            // LDPC_XR: XCD-resident BP decoder for array codes (kernels_xr.hpp)
+constexpr int64_t kDefaultXrK = 3;           // LDPC_XR_K: its slots (codewords in flight) per XCD
+constexpr int64_t kDefaultXrVb = 4;          // LDPC_XR_VB: column blocks per variable task (1, 2, 4)
+constexpr int64_t kDefaultXrLdm = 1;         // LDPC_XR_LDM: L1-bypassing loads, 1 nontemporal, 2 agent scope
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
@@ -95,6 +101,8 @@ Engine::~Engine()
     hipFree(d_unsat); hipFree(d_done); hipFree(d_fin); hipFree(d_fin_b); hipFree(d_fin_n);
     hipFree(v2c); if (c2v != v2c) hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
     hipFree(post_t);
+    hipFree(d_xr_jpb); hipFree(d_xr_ord4); hipFree(d_xr_inv8); hipFree(d_xr_col); hipFree(xr_msg); hipFree(xr_prior); hipFree(xr_post);
+    hipFree(xr_hb); hipFree(xr_ctl); hipFree(xr_next);
     if (stream) hipStreamDestroy(stream);
     if (stream2) hipStreamDestroy(stream2);
 }
@@ -131,6 +139,16 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     if (nt < 0) nt = (int)env_int("LDPC_NT_D", kDefaultNT);
     const bool reg_72_8 = g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
     msa_c = algo == LDPC_ALGO_MSA && reg_72_8 && nt != 0 && g->N % 16 == 0 && env_int("LDPC_MSA_C", kDefaultMsaC) != 0;
+    // XCD-resident decoder: array codes (block structure found) with the
+    // instantiated degrees; everything below is then only a small fallback state
+    if (algo == LDPC_ALGO_BP && reg_72_8 && env_int("LDPC_XR", kDefaultXr) != 0 && (xr_layout = xr_layout_of(*g))) {
+        const int rc = init_xr();
+        if (rc) return rc;
+        if (xr) {
+            res_mode = 0;
+            chunk = 64;
+        }
+    }
     if (cont_mode < 0) cont_mode = (int)env_int("LDPC_CONT", kDefaultCont);
     cont = cont_mode != 0 && !int_algo && reg_72_8;
     // resident pool: a few tiles whose whole state fits the
@@ -880,6 +898,7 @@ int Engine::decode(const double* d_in, int in_kind, int64_t B, int32_t max_iter,
         }
         return LDPC_OK;
     }
+    if (xr) return run_xr(d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
     if (cont) return run_cont(d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
     // balanced passes of <= cap codewords (multiples of 64 except the tail)
     const int64_t npass = (B + cap - 1) / cap;
@@ -891,6 +910,123 @@ int Engine::decode(const double* d_in, int in_kind, int64_t B, int32_t max_iter,
                            d_post ? d_post + (size_t)b0 * N : nullptr, post_kind, d_iters ? d_iters + b0 : nullptr,
                            d_valid ? d_valid + b0 : nullptr);
         if (rc) return rc;
+    }
+    return LDPC_OK;
+}
+
+// XCD-resident decoder (kernels_xr.hpp): probe the XCDs, then the slots'
+// state (K per XCD, ~1.33 MB each for the DNA code) and the block tables.
+int Engine::init_xr()
+{
+    int cus = 0;
+    LDPC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    const int nb = 8 * std::max(cus, 1);
+    unsigned* d_x = nullptr;
+    LDPC_HIP(hipMalloc((void**)&d_x, (size_t)nb * sizeof(unsigned)));
+    hipLaunchKernelGGL(dev::k_xr_probe, dim3(nb), dim3(64), 0, stream, d_x);
+    std::vector<unsigned> hx((size_t)nb);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(hx.data(), d_x, (size_t)nb * sizeof(unsigned), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    hipFree(d_x);
+    if (e != hipSuccess) { set_error(std::string("XCD probe: ") + hipGetErrorString(e)); return LDPC_ERR_DEVICE; }
+    unsigned mx = 0;
+    for (unsigned v : hx) mx = std::max(mx, v);
+    std::vector<int> seen(mx + 1, 0);
+    for (unsigned v : hx) seen[v]++;
+    for (int v : seen)
+        if (v == 0) return LDPC_OK;  // ids not dense: keep the tiled decoders (xr stays off)
+    xr_nxcd = (int)mx + 1;
+    xr_k = (int)std::max<int64_t>(1, std::min<int64_t>(env_int("LDPC_XR_K", kDefaultXrK), 64));
+    xr_vb = (int)env_int("LDPC_XR_VB", kDefaultXrVb);
+    if (xr_vb != 1 && xr_vb != 2) xr_vb = 4;
+    xr_grid = (int)env_int("LDPC_XR_GRID", cus);
+    if (xr_grid <= 0) xr_grid = cus;
+    const XrLayout& L = *xr_layout;
+    const size_t S = (size_t)xr_nxcd * xr_k, E = (size_t)g->E, N = (size_t)g->N;
+    int rc;
+    if ((rc = upload(&d_xr_jpb, L.jpb)) || (rc = upload(&d_xr_ord4, L.ord4)) || (rc = upload(&d_xr_inv8, L.inv8)) || (rc = upload(&d_xr_col, L.col_orig)))
+        return rc;
+    LDPC_HIP(hipMalloc((void**)&xr_msg, S * E * sizeof(double)));
+    LDPC_HIP(hipMalloc((void**)&xr_prior, S * N * sizeof(double)));
+    LDPC_HIP(hipMalloc((void**)&xr_hb, S * (N / 64) * sizeof(uint64_t)));
+    LDPC_HIP(hipMalloc((void**)&xr_ctl, S * sizeof(dev::XrCtl)));
+    LDPC_HIP(hipMalloc((void**)&xr_next, sizeof(unsigned long long)));
+    xr = true;
+    return LDPC_OK;
+}
+
+// One persistent launch decodes the whole batch: each XCD's workgroups run the
+// check / variable tasks of that XCD's slots, each slot claiming codewords
+// from the batch as it finishes one (kernels_xr.hpp).
+int Engine::run_xr(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
+                   int post_kind, int32_t* d_iters, uint8_t* d_valid)
+{
+    using namespace dev;
+    if (!d_hard || !d_iters || !d_valid) { set_error("the XCD-resident decoder needs hard, iters and valid outputs"); return LDPC_ERR_ARG; }
+    const int S = xr_nxcd * xr_k;
+    const size_t N = (size_t)g->N;
+    if (d_post && !xr_post) LDPC_HIP(hipMalloc((void**)&xr_post, (size_t)S * N * sizeof(double)));
+    hipLaunchKernelGGL(k_xr_reset, dim3(1), dim3(256), 0, stream, xr_ctl, S, xr_next);
+    LDPC_HIP(hipGetLastError());
+    XrArgs a{};
+    a.jpb = d_xr_jpb;
+    a.ord4 = d_xr_ord4;
+    a.inv8 = d_xr_inv8;
+    a.col_orig = d_xr_col;
+    a.Q = xr_layout->Q;
+    a.N = g->N;
+    a.E = g->E;
+    a.msg = xr_msg;
+    a.prior = xr_prior;
+    a.post = d_post ? xr_post : nullptr;
+    a.hb = xr_hb;
+    a.ctl = xr_ctl;
+    a.K = xr_k;
+    a.nxcd = xr_nxcd;
+    a.in = d_in;
+    a.in_is_llr = in_kind == LDPC_IN_LLR ? 1 : 0;
+    a.max_iter = max_iter;
+    a.B = B;
+    a.next_b = xr_next;
+    a.hard_out = d_hard;
+    a.post_out = d_post;
+    a.post_ratio = post_kind == LDPC_POST_RATIO ? 1 : 0;
+    a.iters_out = d_iters;
+    a.valid_out = d_valid;
+    unsigned long long* prof = nullptr;
+    if (env_int("LDPC_XR_PROF", 0)) {
+        LDPC_HIP(hipMalloc((void**)&prof, (size_t)xr_grid * 16 * sizeof(unsigned long long)));
+        LDPC_HIP(hipMemsetAsync(prof, 0, (size_t)xr_grid * 16 * sizeof(unsigned long long), stream));
+    }
+    a.prof = prof;
+#define XR_LAUNCH(VB, LDM) \
+    LAUNCH_ON(stream, K_CHECK, hipLaunchKernelGGL((k_xr_bp<72, 8, VB, LDM>), dim3(xr_grid), dim3(256), 0, stream, a))
+    const int ldm = (int)env_int("LDPC_XR_LDM", kDefaultXrLdm);
+    if (xr_vb == 4 && ldm == 1) XR_LAUNCH(4, 1);
+    else if (xr_vb == 4) XR_LAUNCH(4, 2);
+    else if (xr_vb == 1 && ldm == 1) XR_LAUNCH(1, 1);
+    else if (xr_vb == 1) XR_LAUNCH(1, 2);
+    else if (ldm == 0) XR_LAUNCH(2, 0);
+    else if (ldm == 1) XR_LAUNCH(2, 1);
+    else XR_LAUNCH(2, 2);
+#undef XR_LAUNCH
+    if (prof) {  // debug: per-workgroup cycle split, summed, to stderr
+        std::vector<unsigned long long> h((size_t)xr_grid * 16);
+        LDPC_HIP(hipMemcpyAsync(h.data(), prof, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+        LDPC_HIP(hipStreamSynchronize(stream));
+        hipFree(prof);
+        unsigned long long t[16] = {0};
+        for (int b = 0; b < xr_grid; b++)
+            for (int q = 0; q < 16; q++) t[q] += h[(size_t)b * 16 + q];
+        const double tot = (double)(t[0] + t[1] + t[3] + t[5]);
+        std::fprintf(stderr,
+                     "xr prof B=%lld K=%d grid=%d: claim %.3f check %.3f (%llu, %.0f cyc) var %.3f (%llu, %.0f cyc) "
+                     "done+book %.3f (%llu bookkeepings); check split load %.0f compute %.0f rest %.0f cyc\n",
+                     (long long)B, xr_k, xr_grid, t[0] / tot, t[1] / tot, t[2], t[2] ? (double)t[1] / t[2] : 0.0,
+                     t[3] / tot, t[4], t[4] ? (double)t[3] / t[4] : 0.0, t[5] / tot, t[6],
+                     t[2] ? (double)t[8] / t[2] : 0.0, t[2] ? (double)t[9] / t[2] : 0.0,
+                     t[2] ? (double)(t[1] - t[8] - t[9]) / t[2] : 0.0);
     }
     return LDPC_OK;
 }

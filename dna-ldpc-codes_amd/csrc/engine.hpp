@@ -112,6 +112,23 @@ struct Engine {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> wall_live;
     double wall_ms = 0;
     int64_t wall_runs = 0;
+    // XCD-resident BP decoder (kernels_xr.hpp, LDPC_XR): array codes only
+    bool xr = false;
+    int xr_k = 3;           // slots (codewords in flight) per XCD
+    int xr_vb = 2;          // column blocks per variable task
+    int xr_nxcd = 0;        // XCDs (probed from HW_REG_XCC_ID)
+    int xr_grid = 0;        // persistent workgroups
+    const XrLayout* xr_layout = nullptr;
+    uint8_t* d_xr_jpb = nullptr;
+    uint32_t* d_xr_ord4 = nullptr;
+    uint64_t* d_xr_inv8 = nullptr;
+    int32_t* d_xr_col = nullptr;
+    double* xr_msg = nullptr;
+    double* xr_prior = nullptr;
+    double* xr_post = nullptr;
+    uint64_t* xr_hb = nullptr;
+    dev::XrCtl* xr_ctl = nullptr;
+    unsigned long long* xr_next = nullptr;
 
     ~Engine();
     int init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, int64_t group = -1, int nt = -1,
@@ -141,6 +158,9 @@ struct Engine {
     int launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt, const dev::Refill& rf);
     int launch_pingpong(hipStream_t s, int64_t tc, int64_t tv, double* pt, const dev::ResStep& rs,
                         const dev::Refill& rf);
+    int init_xr();
+    int run_xr(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
+               int post_kind, int32_t* d_iters, uint8_t* d_valid);
 };
 
 // bytes of device memory per resident codeword

@@ -462,4 +462,107 @@ int build_rs_ldpc(int s, int rho, int gamma, HostGraph& g, std::vector<int>* gen
     return build_graph(M, N, rows.data(), cols.data(), (int64_t)rows.size(), g, msg);
 }
 
+namespace {
+
+// cls[j] = column block of column j: every row must hold exactly one column of
+// every block, and every block Q columns
+bool check_col_blocks(const HostGraph& g, const std::vector<int32_t>& cls, int32_t RB, int32_t Q)
+{
+    std::vector<int32_t> cnt((size_t)RB, 0);
+    for (int32_t j = 0; j < g.N; j++) {
+        if (cls[(size_t)j] < 0 || cls[(size_t)j] >= RB) return false;
+        cnt[(size_t)cls[(size_t)j]]++;
+    }
+    for (int32_t b = 0; b < RB; b++)
+        if (cnt[(size_t)b] != Q) return false;
+    std::vector<int32_t> seen((size_t)RB, -1);
+    for (int32_t i = 0; i < g.M; i++)
+        for (int32_t e = g.row_ptr[(size_t)i]; e < g.row_ptr[(size_t)i + 1]; e++) {
+            const int32_t b = cls[(size_t)g.col_idx[(size_t)e]];
+            if (seen[(size_t)b] == i) return false;
+            seen[(size_t)b] = i;
+        }
+    return true;
+}
+
+}  // namespace
+
+bool find_xr_layout(const HostGraph& g, XrLayout& L)
+{
+    if (!g.regular_dv || !g.regular_dc || g.dv_max < 1 || g.dv_max > 8 || g.dc_max < 2) return false;
+    const int32_t GA = g.dv_max, RB = g.dc_max;
+    if (g.M % GA != 0) return false;
+    const int32_t Q = g.M / GA;
+    if (Q % 64 != 0 || Q > 256 || (int64_t)g.N != (int64_t)RB * Q) return false;
+    // row blocks: rows a*Q .. a*Q+Q-1 cover every column exactly once
+    std::vector<int32_t> seen((size_t)g.N, -1);
+    for (int32_t i = 0; i < g.M; i++)
+        for (int32_t e = g.row_ptr[(size_t)i]; e < g.row_ptr[(size_t)i + 1]; e++) {
+            const int32_t j = g.col_idx[(size_t)e];
+            if (seen[(size_t)j] == i / Q) return false;
+            seen[(size_t)j] = i / Q;
+        }
+    // column blocks: contiguous blocks of Q columns, else the blocks of the
+    // RS-LDPC code (build_rs_ldpc) with the same rows, matched by row sets
+    std::vector<int32_t> cls((size_t)g.N);
+    for (int32_t j = 0; j < g.N; j++) cls[(size_t)j] = j / Q;
+    if (!check_col_blocks(g, cls, RB, Q)) {
+        int s = 0;
+        while ((1 << s) < Q) s++;
+        HostGraph rs;
+        if ((1 << s) != Q || build_rs_ldpc(s, RB, GA, rs, nullptr, nullptr, nullptr) != LDPC_OK) return false;
+        if (rs.M != g.M || rs.N != g.N) return false;
+        std::map<std::vector<int32_t>, int32_t> key;
+        std::vector<int32_t> k((size_t)GA);
+        for (int32_t j = 0; j < rs.N; j++) {
+            for (int32_t s2 = 0; s2 < GA; s2++)
+                k[(size_t)s2] = rs.edge_row[(size_t)rs.col_edge[(size_t)rs.col_ptr[(size_t)j] + s2]];
+            key[k] = j;
+        }
+        for (int32_t j = 0; j < g.N; j++) {
+            for (int32_t s2 = 0; s2 < GA; s2++)
+                k[(size_t)s2] = g.edge_row[(size_t)g.col_edge[(size_t)g.col_ptr[(size_t)j] + s2]];
+            auto it = key.find(k);
+            if (it == key.end()) return false;
+            cls[(size_t)j] = it->second / Q;
+        }
+        if (!check_col_blocks(g, cls, RB, Q)) return false;
+    }
+    // position of each column inside its block (ascending column index)
+    std::vector<int32_t> jp((size_t)g.N), fill((size_t)RB, 0);
+    for (int32_t j = 0; j < g.N; j++) jp[(size_t)j] = fill[(size_t)cls[(size_t)j]]++;
+    L.Q = Q;
+    L.GA = GA;
+    L.RB = RB;
+    const int32_t RW = (RB + 3) / 4;
+    L.jpb.assign((size_t)GA * RB * Q, 0);
+    L.ord4.assign((size_t)GA * RW * Q, 0);
+    L.inv8.assign((size_t)RB * Q, 0);
+    L.col_orig.assign((size_t)RB * Q, 0);
+    for (int32_t i = 0; i < g.M; i++) {
+        const int32_t a = i / Q, r = i % Q;
+        for (int32_t e = g.row_ptr[(size_t)i]; e < g.row_ptr[(size_t)i + 1]; e++) {
+            const int32_t j = g.col_idx[(size_t)e], b = cls[(size_t)j];
+            const int32_t rank = e - g.row_ptr[(size_t)i];  // position in the row's column order
+            L.jpb[((size_t)a * RB + b) * Q + r] = (uint8_t)jp[(size_t)j];
+            L.ord4[((size_t)a * RW + rank / 4) * Q + r] |= (uint32_t)b << (8 * (rank % 4));
+            L.inv8[(size_t)b * Q + jp[(size_t)j]] |= (uint64_t)r << (8 * a);
+            L.col_orig[(size_t)b * Q + jp[(size_t)j]] = j;
+        }
+    }
+    return true;
+}
+
+const XrLayout* xr_layout_of(const HostGraph& g)
+{
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (g.xr_state == 0) {
+        auto L = std::make_shared<XrLayout>();
+        g.xr_state = find_xr_layout(g, *L) ? 1 : -1;
+        if (g.xr_state > 0) g.xr_cache = L;
+    }
+    return g.xr_state > 0 ? g.xr_cache.get() : nullptr;
+}
+
 }  // namespace ldpc

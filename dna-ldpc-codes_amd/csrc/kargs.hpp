@@ -63,5 +63,52 @@ struct ResStep {
     ContOut co;                  // iters / valid (hard / post are written by k_var_m)
 };
 
+// XCD-resident BP decoder (kernels_xr.hpp)
+constexpr uint32_t XR_DEAD = 0xFFFFFFFFu;
+enum : unsigned long long { XR_LIVE = 1, XR_FIN = 2, XR_FRESH = 4 };
+// packed slot state: codeword (40 bits, all ones = none) | iterations << 40 | mode << 56
+constexpr unsigned long long XR_CW_MASK = (1ull << 40) - 1, XR_NO_CW = XR_CW_MASK;
+__host__ __device__ constexpr unsigned long long xr_state(unsigned long long cw, unsigned long long n,
+                                                          unsigned long long mode)
+{
+    return (cw & XR_CW_MASK) | ((n & 0xffffull) << 40) | (mode << 56);
+}
+
+// one slot's control words (128 B apart); only atomics touch them
+struct XrCtl {
+    unsigned long long ctl;    // (phase << 32) | tasks claimed
+    unsigned long long done;   // tasks finished since the decode began (monotone)
+    unsigned long long unsat;  // the last check phase that found an unsatisfied row (atomicMax)
+    unsigned long long state;  // xr_state(codeword held, its iterations, variable-phase mode)
+    unsigned long long fin;    // XR_FIN: xr_state(finished codeword, its iterations, 0)
+    unsigned long long pad[11];
+};
+
+struct XrArgs {
+    const uint8_t* jpb;       // [GA][RB][Q]
+    const uint32_t* ord4;     // [GA][(RB+3)/4][Q]
+    const uint64_t* inv8;     // [RB][Q]
+    const int32_t* col_orig;  // [RB][Q]
+    int32_t Q, N;
+    int64_t E;
+    double* msg;              // [S][E]
+    double* prior;            // [S][N]
+    double* post;             // [S][N] per-iteration posterior, or nullptr
+    uint64_t* hb;             // [S][N/64]
+    XrCtl* ctl;               // [S]
+    int32_t K, nxcd;          // slots per XCD, XCDs
+    const double* in;         // [B][N]
+    int32_t in_is_llr;
+    int32_t max_iter;
+    int64_t B;
+    unsigned long long* next_b;
+    uint8_t* hard_out;        // [B][N]
+    double* post_out;         // [B][N] or nullptr
+    int32_t post_ratio;
+    int32_t* iters_out;
+    uint8_t* valid_out;
+    unsigned long long* prof;  // [grid][8] or nullptr (LDPC_XR_PROF)
+};
+
 }  // namespace dev
 }  // namespace ldpc

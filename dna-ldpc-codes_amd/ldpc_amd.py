@@ -76,7 +76,7 @@ _lib_lock = threading.Lock()
 EXPORTS = [
     "ldpc_abi_version", "ldpc_last_error", "ldpc_device_count", "ldpc_graph_load", "ldpc_graph_from_edges",
     "ldpc_graph_load_alist", "ldpc_graph_rs_ldpc", "ldpc_graph_save_pchk", "ldpc_graph_save_alist",
-    "ldpc_graph_free", "ldpc_graph_info", "ldpc_graph_edges", "ldpc_graph_syndrome", "ldpc_decode",
+    "ldpc_graph_free", "ldpc_graph_info", "ldpc_graph_blocks", "ldpc_graph_edges", "ldpc_graph_syndrome", "ldpc_decode",
     "ldpc_engine_create", "ldpc_engine_create_ex", "ldpc_engine_info", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
     "ldpc_engine_gen_bsc", "ldpc_engine_set_params", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_engine_wall", "ldpc_dev_malloc", "ldpc_dev_free",
     "ldpc_dev_memcpy", "ldpc_dna_llr", "ldpc_dna_edit_distance", "ldpc_write_soft_files", "ldpc_py_float_repr",
@@ -112,6 +112,7 @@ def lib():
         L.ldpc_graph_free.restype = None
         L.ldpc_graph_info.argtypes = [vp] + [vp] * 7
         L.ldpc_graph_edges.argtypes = [vp, vp, vp, vp, vp]
+        L.ldpc_graph_blocks.argtypes = [vp, vp, vp, vp, vp]
         L.ldpc_graph_syndrome.argtypes = [vp, vp, vp]
         L.ldpc_decode.argtypes = [vp, vp, i64, i32, i32, vp, vp, vp, vp, C.POINTER(Opts)]
         L.ldpc_engine_create.argtypes = [vp, i32, i32, i64, pint]
@@ -254,6 +255,14 @@ class Graph:
         ce = np.zeros(max(self.E, 1), np.int32)
         _check(lib().ldpc_graph_edges(self._h, _ptr(rp), _ptr(ci), _ptr(cp), _ptr(ce)))
         return rp, ci[: self.E], cp, ce[: self.E]
+
+    def blocks(self):
+        """Array-code block structure (ldpc_graph_blocks): (Q, row_blocks,
+        col_blocks, col_block[N]) or None when H has none."""
+        Q, rb, cb = C.c_int32(), C.c_int32(), C.c_int32()
+        cls = np.full(self.N, -1, np.int32)
+        _check(lib().ldpc_graph_blocks(self._h, C.byref(Q), C.byref(rb), C.byref(cb), _ptr(cls)))
+        return None if Q.value == 0 else (Q.value, rb.value, cb.value, cls)
 
     def syndrome(self, dblk: np.ndarray):
         """Number of unsatisfied checks and the parity vector (check.cpp:28-45)."""
@@ -453,6 +462,7 @@ class Engine:
         self.syndrome_fused = bool(fl.value & 128)  # syndrome in the grouped check launches (LDPC_SYN_FUSED)
         self.tile_streams = bool(fl.value & 256)  # resident pool, one stream per tile (LDPC_RES_STREAMS)
         self.pingpong = bool(fl.value & 512)  # resident BP pool, check(t) + variable(t-1) per launch (LDPC_PINGPONG)
+        self.xcd_resident = bool(fl.value & 1024)  # one persistent launch, slots in the XCDs' L2 (LDPC_XR)
 
     def decode(self, d_in, in_kind: int, B: int, max_iter: int, d_hard=None, d_post=None, post_kind=POST_LLR,
                d_iters=None, d_valid=None):

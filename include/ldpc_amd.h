@@ -128,6 +128,16 @@ void ldpc_graph_free(ldpc_graph *g);
 int ldpc_graph_info(const ldpc_graph *g, int32_t *M, int32_t *N, int64_t *E, int32_t *dv_max,
                     int32_t *regular_dv, int32_t *dc_max, int32_t *regular_dc);
 
+/* Block structure of array codes (RS-LDPC, quasi-cyclic): H is row_blocks x
+ * col_blocks permutation matrices of size Q, rows in contiguous blocks.  Q = 0
+ * when H has no such structure (then only the tiled decoders run).
+ * col_block[N] (may be NULL) receives each column's block.  The column blocks
+ * are found as contiguous runs of Q columns or, for RS-LDPC codes with
+ * permuted columns (the DNA code), by matching the column row sets against
+ * ldpc_graph_rs_ldpc(log2 Q, col_blocks, row_blocks). */
+int ldpc_graph_blocks(const ldpc_graph *g, int32_t *Q, int32_t *row_blocks, int32_t *col_blocks,
+                      int32_t *col_block);
+
 /* Copy out the CSR/CSC edge arrays (row_ptr[M+1], col_idx[E], col_ptr[N+1],
  * col_edge[E]); any pointer may be NULL. */
 int ldpc_graph_edges(const ldpc_graph *g, int32_t *row_ptr, int32_t *col_idx, int32_t *col_ptr,
@@ -220,7 +230,9 @@ int ldpc_engine_set_params(ldpc_engine *e, int32_t msa_precision, double msa_ste
  * continuous-mode syndrome spread over several blocks per tile (env
  * LDPC_SYN_SPLIT); bit 7 = syndrome fused into the grouped check launches
  * (env LDPC_SYN_FUSED); bit 8 = resident pool with one HIP stream per pool
- * tile (env LDPC_RES_STREAMS; the tiles' kernels run concurrently). */
+ * tile (env LDPC_RES_STREAMS; the tiles' kernels run concurrently); bit 9 =
+ * resident BP pool, ping-pong launches (env LDPC_PINGPONG); bit 10 = the
+ * XCD-resident BP decoder for array codes (env LDPC_XR). */
 int ldpc_engine_info(ldpc_engine *e, int64_t *cap, int64_t *group_tiles, int32_t *flags);
 int ldpc_engine_stats(ldpc_engine *e, ldpc_kernel_stats *out);
 /* Device time of whole decodes with concurrent tile streams (bit 8 of

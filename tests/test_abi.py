@@ -124,3 +124,26 @@ def test_cli_rejects_bad_argc():
     exe = os.path.join(ROOT, "dna-ldpc-codes_amd", "bin", "ldpc")
     r = subprocess.run([exe, "0", "0", "0"], capture_output=True, text=True)
     assert r.returncode == 1 and "argc error!" in r.stderr
+
+
+def test_graph_blocks_array_structure(L):
+    """ldpc_graph_blocks: the DNA code is RS-LDPC(8, 72, 8) with permuted
+    columns; its column blocks are found by row-set matching and equal the RS
+    blocks of the committed column permutation (tests/golden/code_fixtures.npz).
+    Codes built in natural order get contiguous blocks; graphs without the
+    structure (irregular, Q < 64) report none."""
+    from conftest import GOLDEN
+    G = L.Graph(PCHK)
+    Q, rb, cb, cls = G.blocks()
+    assert (Q, rb, cb) == (256, 8, 72)
+    perm = np.load(os.path.join(GOLDEN, "code_fixtures.npz"))["rs_big_colperm"]
+    assert np.array_equal(cls, perm // 256)
+    rp, ci, _, _ = G.edges()
+    rows = ci.reshape(G.M, G.dc)
+    assert (np.sort(cls[rows], axis=1) == np.arange(72)).all()  # one column of every block per row
+    R = L.Graph.rs_ldpc(7, 72, 8)
+    Q, rb, cb, cls = R.blocks()
+    assert (Q, rb, cb) == (128, 8, 72) and np.array_equal(cls, np.arange(R.N) // 128)
+    assert L.Graph.rs_ldpc(5, 16, 4).blocks() is None  # Q = 32
+    irr = L.Graph.from_edges(4, 6, [0, 0, 1, 1, 2, 3], [0, 1, 2, 3, 4, 5])
+    assert irr.blocks() is None
