@@ -18,6 +18,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                                    \
@@ -84,6 +85,20 @@ int main(int argc, char** argv)
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
+    if (argc > 1 && std::string(argv[1]) == "calib") {
+        // PMC calibration (tools/gpu_pmc_r2.sh): one in-place pass of the check
+        // kernel's shape (72 x 512 B read, then rewritten, per wave) over 2048 MB
+        // (HBM) and over 64 MB (Infinity Cache after the first pass): known
+        // bytes, 2048 / 64 MB read and the same written, per dispatch
+        for (double mb : {2048.0, 64.0}) {
+            const size_t nw = (size_t)(mb * (1 << 20)) / 512 / 72;
+            for (int r = 0; r < 3; r++)
+                hipLaunchKernelGGL(rows_rmw<72>, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, 0, a, nw, 1);
+            CK(hipDeviceSynchronize());
+            std::printf("calib %.0f MB: %zu waves, %.0f bytes read + written per dispatch\n", mb, nw, (double)nw * 72 * 512);
+        }
+        return 0;
+    }
     const double mbs[] = {4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256, 320, 512, 2048};
     std::printf("cus %d\n", cus);
     std::printf("%8s %10s %10s %10s %10s %10s %10s\n", "MB", "rows72_l", "rows72_p", "rows8_l", "rows8_p", "cols_l",
