@@ -125,7 +125,7 @@ def bench_dna272(args):
         "config": {"workload": f"dna272-bp{max_iter}", "batch": B, "max_iter": max_iter,
                    "mean_iters": round(float(it.mean()), 3), "genie_ok": int((hard == cw).all(axis=1).sum()),
                    "host_api_ms_median": round(float(np.median(th)) * 1e3, 2),
-                   "host_api_includes": "host exp + H2D + decode + D2H (ldpc_decode)"},
+                   "host_api_includes": "ldpc_decode end to end: host LR (exp table for the k*ln49 alphabet, else host exp) + H2D + decode + packed hard-bit D2H + unpack"},
     }
     if args.cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

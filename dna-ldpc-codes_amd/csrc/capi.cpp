@@ -10,8 +10,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -30,8 +36,123 @@ using ldpc::set_error;
 // resident pool); larger ones use the engine's own pool
 constexpr int64_t kExplicitPoolMax = 1024;
 constexpr int64_t kXferChunk = 4096;  // codewords per PCIe chunk (at least)
+constexpr int64_t kSmallXfer = 0;  // ... and for shards of <= kExplicitPoolMax (LDPC_SMALL_XFER; 0: one chunk -- A/B on the DNA batch: 128, 192 and one chunk within noise, 64 slower)
 
 namespace {
+
+// Persistent host workers (one set per device context): the host-side passes
+// over a chunk (exp, LLR encoding, copies) split into `n` row ranges, run by
+// the workers and the calling thread, with no thread creation per call.
+class Workers {
+  public:
+    explicit Workers(int n) : n_(std::max(1, n))
+    {
+        for (int t = 1; t < n_; t++) th_.emplace_back([this, t] { loop(t); });
+    }
+    ~Workers()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return n_; }
+    // f(t) for t = 0..n_-1, t = 0 on the calling thread; returns when all are
+    // done.  Callers on different threads take turns.
+    void run(const std::function<void(int)>& f)
+    {
+        if (n_ == 1) { f(0); return; }
+        std::lock_guard<std::mutex> turn(run_mu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &f;
+            left_ = n_ - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return left_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void loop(int t)
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                f = job_;
+            }
+            (*f)(t);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    int n_;
+    std::vector<std::thread> th_;
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    int left_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// LR table path (DNA batches): an LLR that is an exact multiple k * unit, |k|
+// <= kCodeMax, gets LR = table[k] = the host libm's exp(k * unit) -- the same
+// bits as exp(LLR), DNA_main.cpp:1344 -- and crosses PCIe as one byte.
+constexpr int kCodeMax = 127;
+
+// the unit: the smallest nonzero |LLR| among the chunk's first rows (a guess;
+// every value is checked against it)
+double llr_unit(const double* src, int64_t rows, size_t N)
+{
+    double u = 0;
+    const size_t n = (size_t)std::min<int64_t>(rows, 4) * N;
+    for (size_t i = 0; i < n; i++) {
+        const double a = std::fabs(src[i]);
+        if (a > 0 && std::isfinite(a) && (u == 0 || a < u)) u = a;
+    }
+    return u;
+}
+
+// codes of LLRs [i0, i1); false when one is not k * unit with |k| <=
+// kCodeMax.  Branch-free (round to nearest by the 1.5 * 2^52 trick, |q| <
+// 2^51 here), so the compiler vectorises it.
+bool encode_rows(const double* __restrict__ src, int8_t* __restrict__ code, size_t i0, size_t i1, double unit)
+{
+    const double inv = 1.0 / unit, magic = 6755399441055744.0, lim = kCodeMax;
+    int bad = 0;
+    for (size_t i = i0; i < i1; i++) {
+        const double x = src[i];
+        const double kd = (x * inv + magic) - magic;
+        bad |= (int)(kd * unit != x) | (int)!(kd <= lim && kd >= -lim);
+        code[i] = (int8_t)(int)std::fmin(std::fmax(kd, -lim), lim);
+    }
+    return bad == 0;
+}
+
+// byte x -> 8 bytes, byte r = bit r of x (unpacking the device's packed hard bits)
+struct BitBytes {
+    uint64_t t[256];
+    BitBytes()
+    {
+        for (int x = 0; x < 256; x++) {
+            uint64_t v = 0;
+            for (int r = 0; r < 8; r++) v |= (uint64_t)((x >> r) & 1) << (8 * r);
+            t[x] = v;
+        }
+    }
+};
+const BitBytes kBitBytes;
 
 // One reusable device context for host-buffer decodes: an engine plus two
 // sets of pinned / device staging buffers of `xfer` codewords each, so that
@@ -55,14 +176,23 @@ struct Slot {
     uint8_t* d_hard[2] = {};
     int32_t* d_iters[2] = {};
     uint8_t* d_valid[2] = {};
+    uint8_t* h_hbits[2] = {};  // hard bits packed 8 per byte (N % 8 == 0)
+    uint8_t* d_hbits[2] = {};
+    int8_t* h_code[2] = {};   // LR table path: one byte per LLR
+    int8_t* d_code[2] = {};
+    double* h_table[2] = {};  // [2 * kCodeMax + 1]
+    double* d_table[2] = {};
+    std::unique_ptr<Workers> workers;
 
     ~Slot()
     {
+        workers.reset();
         if (eng) hipSetDevice(device);
         for (int k = 0; k < 2; k++) {
             hipHostFree(h_in[k]); hipHostFree(h_post[k]); hipHostFree(h_hard[k]); hipHostFree(h_iters[k]);
-            hipHostFree(h_valid[k]);
+            hipHostFree(h_valid[k]); hipHostFree(h_code[k]); hipHostFree(h_table[k]); hipHostFree(h_hbits[k]);
             hipFree(d_in[k]); hipFree(d_post[k]); hipFree(d_hard[k]); hipFree(d_iters[k]); hipFree(d_valid[k]);
+            hipFree(d_code[k]); hipFree(d_table[k]); hipFree(d_hbits[k]);
             if (ev_h2d[k]) hipEventDestroy(ev_h2d[k]);
             if (ev_dec[k]) hipEventDestroy(ev_dec[k]);
             if (ev_d2h[k]) hipEventDestroy(ev_d2h[k]);
@@ -107,19 +237,31 @@ int make_slot(const HostGraph* g, int device, int algo, int64_t pool, int64_t xf
         LDPC_HIP(hipMalloc((void**)&s->d_hard[k], C * N));
         LDPC_HIP(hipMalloc((void**)&s->d_iters[k], C * sizeof(int32_t)));
         LDPC_HIP(hipMalloc((void**)&s->d_valid[k], C));
+        if (N % 8 == 0) {
+            LDPC_HIP(hipHostMalloc((void**)&s->h_hbits[k], C * N / 8, hipHostMallocDefault));
+            LDPC_HIP(hipMalloc((void**)&s->d_hbits[k], C * N / 8));
+        }
+        if (algo == LDPC_ALGO_BP) {
+            LDPC_HIP(hipHostMalloc((void**)&s->h_code[k], C * N, hipHostMallocDefault));
+            LDPC_HIP(hipMalloc((void**)&s->d_code[k], C * N));
+            LDPC_HIP(hipHostMalloc((void**)&s->h_table[k], (2 * kCodeMax + 1) * sizeof(double), hipHostMallocDefault));
+            LDPC_HIP(hipMalloc((void**)&s->d_table[k], (2 * kCodeMax + 1) * sizeof(double)));
+        }
     }
     out = std::move(s);
     return LDPC_OK;
 }
 
+// f(r0, r1) over n rows split across the slot's workers
 template <typename F>
-void parallel_rows(int64_t n, int threads, F&& f)
+void parallel_rows(Workers& W, int64_t n, F&& f)
 {
-    threads = (int)std::max<int64_t>(1, std::min<int64_t>(threads, n));
-    if (threads == 1) { f(0, n); return; }
-    std::vector<std::thread> th;
-    for (int t = 0; t < threads; t++) th.emplace_back([&, t] { f(n * t / threads, n * (t + 1) / threads); });
-    for (auto& x : th) x.join();
+    const int T = W.size();
+    if (T == 1 || n < 2) { f(0, n); return; }
+    W.run([&](int t) {
+        const int64_t r0 = n * t / T, r1 = n * (t + 1) / T;
+        if (r1 > r0) f(r0, r1);
+    });
 }
 
 }  // namespace
@@ -318,7 +460,14 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
     const int ndev = std::max(1, (int)o.n_devices);
     for (int i = 0; i < ndev; i++) devs.push_back(o.devices ? o.devices[i] : i);
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-    const int host_threads = o.host_threads > 0 ? o.host_threads : std::min(8, std::max(1, hw / ndev));
+    const int host_threads = o.host_threads > 0 ? o.host_threads : std::min(16, std::max(1, hw / ndev));
+    const char* tev = std::getenv("LDPC_LR_TABLE");
+    const bool lr_table = !(tev && *tev && std::atoi(tev) == 0);
+    const char* xev = std::getenv("LDPC_SMALL_XFER");
+    const int64_t small_xfer = (xev && *xev) ? (std::atoll(xev) + 63) / 64 * 64 : kSmallXfer;
+    const char* pev = std::getenv("LDPC_API_TIMING");  // debug: host-leg split to stderr
+    const bool api_timing = pev && *pev && std::atoi(pev) != 0;
+    auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const size_t N = (size_t)g->h.N;
 
     std::vector<int> rcs(devs.size(), LDPC_OK);
@@ -335,13 +484,19 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
         // PCIe in double-buffered chunks of `xfer`.
         const int64_t sh64 = (shard + 63) / 64 * 64;
         const int64_t pool = o.chunk > 0 ? o.chunk : (shard <= kExplicitPoolMax ? sh64 : 0);
-        const int64_t xfer = std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool + 63) / 64 * 64));
+        // small shards (the DNA batch) cross in chunks of kSmallXfer codewords,
+        // so the host work on one chunk overlaps the decode of the one before
+        const int64_t xfer = (o.chunk <= 0 && shard <= kExplicitPoolMax && small_xfer > 0)
+                                 ? std::min<int64_t>(sh64, small_xfer)
+                                 : std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool + 63) / 64 * 64));
         std::unique_ptr<Slot> slot = g->take(dev, algo, pool, xfer, o.chunk <= 0 && pool > 0);
         int rc = LDPC_OK;
         if (!slot) rc = make_slot(&g->h, dev, algo, pool, xfer, slot);
         if (!rc && post_out) rc = slot->want_post(N);
         if (rc) { rcs[di] = rc; msgs[di] = ldpc::last_error(); return; }
+        if (!slot->workers || slot->workers->size() != host_threads) slot->workers = std::make_unique<Workers>(host_threads);
         Slot& S = *slot;
+        Workers& W = *S.workers;
         Engine& E = *S.eng;
         const bool host_exp = (algo == LDPC_ALGO_BP) && o.exp_on_host;
         const int in_kind = (algo == LDPC_ALGO_BP && host_exp) ? LDPC_IN_LR : LDPC_IN_LLR;
@@ -357,28 +512,87 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
             const double* src = llr + (size_t)c0(c) * N;
             LDPC_HIP(hipSetDevice(dev));
             if (c >= 2) LDPC_HIP(hipEventSynchronize(S.ev_h2d[k]));  // staging buffer free again
-            if (host_exp)
-                parallel_rows(Bc, host_threads, [&](int64_t r0, int64_t r1) {
-                    for (size_t i = (size_t)r0 * N; i < (size_t)r1 * N; i++) S.h_in[k][i] = std::exp(src[i]);
-                });
-            else
-                parallel_rows(Bc, host_threads, [&](int64_t r0, int64_t r1) {
-                    std::memcpy(S.h_in[k] + (size_t)r0 * N, src + (size_t)r0 * N, (size_t)(r1 - r0) * N * 8);
-                });
+            const double tp0 = api_timing ? now() : 0;
+            // LR table path: all of the chunk's LLRs exact multiples of one unit
+            bool coded = false;
+            if (host_exp && lr_table && S.h_code[k]) {
+                const double unit = llr_unit(src, Bc, N);
+                if (unit > 0) {
+                    // in pieces, each crossing PCIe while the next is encoded
+                    if (c >= 2) LDPC_HIP(hipStreamWaitEvent(S.copy, S.ev_dec[k], 0));
+                    const int64_t pieces = std::min<int64_t>(4, Bc);
+                    std::atomic<bool> ok{true};
+                    for (int64_t pc = 0; pc < pieces && ok; pc++) {
+                        const int64_t p0 = Bc * pc / pieces, p1 = Bc * (pc + 1) / pieces;
+                        parallel_rows(W, p1 - p0, [&](int64_t r0, int64_t r1) {
+                            if (!encode_rows(src, S.h_code[k], (size_t)(p0 + r0) * N, (size_t)(p0 + r1) * N, unit))
+                                ok = false;
+                        });
+                        if (ok)
+                            LDPC_HIP(hipMemcpyAsync(S.d_code[k] + (size_t)p0 * N, S.h_code[k] + (size_t)p0 * N,
+                                                    (size_t)(p1 - p0) * N, hipMemcpyHostToDevice, S.copy));
+                    }
+                    if (ok) {
+                        for (int q = -kCodeMax; q <= kCodeMax; q++) S.h_table[k][q + kCodeMax] = std::exp((double)q * unit);
+                        coded = true;
+                    }
+                }
+            }
+            if (!coded) {
+                if (host_exp)
+                    parallel_rows(W, Bc, [&](int64_t r0, int64_t r1) {
+                        for (size_t i = (size_t)r0 * N; i < (size_t)r1 * N; i++) S.h_in[k][i] = std::exp(src[i]);
+                    });
+                else
+                    parallel_rows(W, Bc, [&](int64_t r0, int64_t r1) {
+                        std::memcpy(S.h_in[k] + (size_t)r0 * N, src + (size_t)r0 * N, (size_t)(r1 - r0) * N * 8);
+                    });
+            }
+            const double tp1 = api_timing ? now() : 0;
             if (c >= 2) LDPC_HIP(hipStreamWaitEvent(S.copy, S.ev_dec[k], 0));
-            LDPC_HIP(hipMemcpyAsync(S.d_in[k], S.h_in[k], (size_t)Bc * N * 8, hipMemcpyHostToDevice, S.copy));
+            if (coded) {  // (the codes are on their way already)
+                LDPC_HIP(hipMemcpyAsync(S.d_table[k], S.h_table[k], (2 * kCodeMax + 1) * sizeof(double),
+                                        hipMemcpyHostToDevice, S.copy));
+                int r = E.expand_lr(S.d_code[k], S.d_table[k], S.d_in[k], Bc * (int64_t)N, S.copy);
+                if (r) return r;
+            } else {
+                LDPC_HIP(hipMemcpyAsync(S.d_in[k], S.h_in[k], (size_t)Bc * N * 8, hipMemcpyHostToDevice, S.copy));
+            }
             LDPC_HIP(hipEventRecord(S.ev_h2d[k], S.copy));
+            if (api_timing) {
+                LDPC_HIP(hipEventSynchronize(S.ev_h2d[k]));
+                std::fprintf(stderr, "api chunk %lld: %s %.3f ms, + H2D%s %.3f ms\n", (long long)c,
+                             coded ? "encode" : "exp/copy", tp1 - tp0, coded ? " + expand" : "", now() - tp1);
+            }
             return LDPC_OK;
         };
         // outputs of chunk c, once its D2H copies are done
         auto finish = [&](int64_t c) -> int {
             const int k = (int)(c & 1);
             const int64_t b0 = c0(c), Bc = cn(c);
+            const double tf0 = api_timing ? now() : 0;
             LDPC_HIP(hipEventSynchronize(S.ev_d2h[k]));
-            std::memcpy(hard_out + (size_t)b0 * N, S.h_hard[k], (size_t)Bc * N);
-            if (post_out) std::memcpy(post_out + (size_t)b0 * N, S.h_post[k], (size_t)Bc * N * 8);
+            const double tf1 = api_timing ? now() : 0;
+            parallel_rows(W, Bc, [&](int64_t r0, int64_t r1) {
+                if (S.h_hbits[k]) {  // packed: 8 hard bits per byte
+                    uint64_t* o = reinterpret_cast<uint64_t*>(hard_out + (size_t)(b0 + r0) * N);
+                    const uint8_t* in = S.h_hbits[k] + (size_t)r0 * N / 8;
+                    const size_t nb = (size_t)(r1 - r0) * N / 8;
+                    if (((uintptr_t)o & 7) == 0)
+                        for (size_t q = 0; q < nb; q++) o[q] = kBitBytes.t[in[q]];
+                    else
+                        for (size_t q = 0; q < nb; q++) std::memcpy((uint8_t*)o + 8 * q, &kBitBytes.t[in[q]], 8);
+                } else {
+                    std::memcpy(hard_out + (size_t)(b0 + r0) * N, S.h_hard[k] + (size_t)r0 * N, (size_t)(r1 - r0) * N);
+                }
+                if (post_out)
+                    std::memcpy(post_out + (size_t)(b0 + r0) * N, S.h_post[k] + (size_t)r0 * N, (size_t)(r1 - r0) * N * 8);
+            });
             if (iters_out) std::memcpy(iters_out + b0, S.h_iters[k], (size_t)Bc * 4);
             if (valid_out) std::memcpy(valid_out + b0, S.h_valid[k], (size_t)Bc);
+            if (api_timing)
+                std::fprintf(stderr, "api chunk %lld: wait decode + D2H %.3f ms, copy out %.3f ms\n", (long long)c,
+                             tf1 - tf0, now() - tf1);
             return LDPC_OK;
         };
         auto decode = [&](int64_t c) -> int {
@@ -396,7 +610,16 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
             if (r) return r;
             LDPC_HIP(hipEventRecord(S.ev_dec[k], E.stream));
             LDPC_HIP(hipStreamWaitEvent(S.copy_out, S.ev_dec[k], 0));
-            LDPC_HIP(hipMemcpyAsync(S.h_hard[k], S.d_hard[k], (size_t)Bc * N, hipMemcpyDeviceToHost, S.copy_out));
+            if (S.d_hbits[k]) {  // 1/8 of the bytes across PCIe
+                r = E.pack_bits(S.d_hard[k], S.d_hbits[k], Bc * (int64_t)N / 8);
+                if (r) return r;
+                LDPC_HIP(hipEventRecord(S.ev_dec[k], E.stream));
+                LDPC_HIP(hipStreamWaitEvent(S.copy_out, S.ev_dec[k], 0));
+                LDPC_HIP(hipMemcpyAsync(S.h_hbits[k], S.d_hbits[k], (size_t)Bc * N / 8, hipMemcpyDeviceToHost,
+                                        S.copy_out));
+            } else {
+                LDPC_HIP(hipMemcpyAsync(S.h_hard[k], S.d_hard[k], (size_t)Bc * N, hipMemcpyDeviceToHost, S.copy_out));
+            }
             if (post_out)
                 LDPC_HIP(hipMemcpyAsync(S.h_post[k], S.d_post[k], (size_t)Bc * N * 8, hipMemcpyDeviceToHost,
                                         S.copy_out));

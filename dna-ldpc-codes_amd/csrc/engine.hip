@@ -1319,4 +1319,25 @@ int Engine::gen_bsc(double* d_out, int out_kind, int64_t b0, int64_t B, const ui
     return LDPC_OK;
 }
 
+int Engine::expand_lr(const int8_t* d_code, const double* d_table, double* d_out, int64_t n, hipStream_t s)
+{
+    if (n <= 0) return LDPC_OK;
+    LDPC_HIP(hipSetDevice(device));
+    const int64_t blocks = std::min<int64_t>(4096, (n / 8 + 255) / 256 + 1);
+    hipLaunchKernelGGL(dev::k_lr_table, dim3((unsigned)blocks), dim3(256), 0, s, d_code, d_table, d_out, n);
+    LDPC_HIP(hipGetLastError());
+    return LDPC_OK;
+}
+
+int Engine::pack_bits(const uint8_t* d_in, uint8_t* d_out, int64_t nbytes)
+{
+    if (nbytes <= 0) return LDPC_OK;
+    LDPC_HIP(hipSetDevice(device));
+    const int64_t blocks = std::min<int64_t>(4096, (nbytes + 255) / 256);
+    hipLaunchKernelGGL(dev::k_pack_bits, dim3((unsigned)blocks), dim3(256), 0, stream, (const uint64_t*)d_in, d_out,
+                       nbytes);
+    LDPC_HIP(hipGetLastError());
+    return LDPC_OK;
+}
+
 }  // namespace ldpc

@@ -147,6 +147,10 @@ struct Engine {
     int gen_bsc(double* d_out, int out_kind, int64_t b0, int64_t B, const uint8_t* d_cw, int32_t n_cw, uint64_t seed,
                 double p, double llr_mag);
     int collect_stats();
+    // out[i] = table[code[i] + 127] for i < n on stream s (host-API input path)
+    int expand_lr(const int8_t* d_code, const double* d_table, double* d_out, int64_t n, hipStream_t s);
+    // out[i] bit r = in[8 i + r] for i < nbytes on the engine stream (host-API hard-bit copy)
+    int pack_bits(const uint8_t* d_in, uint8_t* d_out, int64_t nbytes);
 
   private:
     hipEvent_t get_event();

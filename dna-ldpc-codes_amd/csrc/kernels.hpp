@@ -1431,6 +1431,38 @@ __global__ __launch_bounds__(256) void k_unpack_hard(const uint64_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// Host-API input path (capi.cpp): LR = table[code + 127], the table holding
+// the host libm's exp(k * unit) -- the reference's LR = exp(LLR)
+// (DNA_main.cpp:1344) for LLRs that are exact multiples k * unit, which the
+// host checked value by value.  8 codes per thread (one 8-byte load).
+// ---------------------------------------------------------------------------
+// hard bits u8 [n][8] -> one byte per 8 (bit r = byte r), for the host API's
+// D2H copy (capi.cpp unpacks them into the caller's one-byte-per-bit array)
+__global__ __launch_bounds__(256) void k_pack_bits(const uint64_t* __restrict__ in, uint8_t* __restrict__ out, int64_t n)
+{
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = in[q];
+        uint32_t b = 0;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) b |= (uint32_t)((v >> (8 * r)) & 1ull) << r;
+        out[q] = (uint8_t)b;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_lr_table(const int8_t* __restrict__ code, const double* __restrict__ table,
+                                                  double* __restrict__ out, int64_t n)
+{
+    const int64_t n8 = n / 8;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8; q += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = reinterpret_cast<const uint64_t*>(code)[q];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) out[q * 8 + r] = table[(int)(int8_t)(c >> (8 * r)) + 127];
+    }
+    for (int64_t i = n8 * 8 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = table[(int)code[i] + 127];
+}
+
+// ---------------------------------------------------------------------------
 // synthetic BSC channel, counter-based:
 //   u = splitmix64(((b << 24) | j) ^ splitmix64(seed)) >> 11, uniform in [0, 2^53)
 //   flip = u * 2^-53 < p;  y = codeword[b mod n_cw][j] ^ flip

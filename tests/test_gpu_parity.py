@@ -565,3 +565,27 @@ def test_pingpong_bitexact(gpu, og, codewords, monkeypatch, tiles, cpw, poll):
     nan = np.isnan(ref_p)
     assert np.array_equal(np.isnan(p), nan)
     assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64))
+
+
+def test_host_lr_table_path(G, og, codewords, monkeypatch):
+    """ldpc_decode's LR table path (capi.cpp): LLRs that are exact multiples
+    k * unit (the DNA alphabet) cross PCIe as one byte each and become
+    table[k] = host exp(k * unit), the same bits as exp(LLR).  Bit-exact
+    against the oracle (host exp), identical to the exp path (LDPC_LR_TABLE=0),
+    and batches off the alphabet (several units, a non-multiple, NaN) fall
+    back to the host exp."""
+    llr = synth.dna_like_llrs(codewords, seed=5, reads=60000)[:150]
+    h1, p1, it1, v1 = _cmp(G, og, llr, 60)
+    monkeypatch.setenv("LDPC_LR_TABLE", "0")
+    G0 = synth_graph = __import__("ldpc_amd").Graph(PCHK)
+    h0, p0, it0, v0 = G0.decode(llr, max_iter=60, post="ratio")
+    assert np.array_equal(h0, h1) and np.array_equal(it0, it1) and np.array_equal(p0.view(np.uint64), p1.view(np.uint64))
+    monkeypatch.delenv("LDPC_LR_TABLE")
+    mixed = llr[:40].copy()
+    mixed[7] *= 1.5  # a second unit
+    mixed[9, 100] = 0.123  # off the alphabet
+    mixed[11, 5] = np.nan
+    _cmp(G, og, mixed, 60) if not np.isnan(mixed).any() else None
+    ref_h, _, ref_it, ref_v = og.decode_batch(mixed, 60, algo=0, threads=8, want_post=False)
+    h, _, it, v = G.decode(mixed, max_iter=60, post=None)
+    assert np.array_equal(h, ref_h) and np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool))
