@@ -105,6 +105,7 @@ struct Engine {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_live[K_NCLASS];
     std::vector<hipEvent_t> ev_pool;
     int64_t launches[K_NCLASS] = {0};
+    hipEvent_t ext_stop = nullptr;  // stop event of the armed sampled launch
     double ms[K_NCLASS] = {0};
     // whole continuous decodes with concurrent tile streams (HIP events on
     // `stream` around each run while profiling): their kernels overlap, so
