@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-2 validation on HEAD: the whole -m gpu suite, smoke, the default
+# bench line, the config 5 line and the DNA batch line.  Each GPU step has its
+# own limit and writes to gpurun_out/<tag>/; a failing step ends the session.
+set -u
+TAG=${1:-r2final}
+R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out/$TAG; mkdir -p "$OUT"; cd "$R"; export TMPDIR=/tmp
+run() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"; local rc=$?; echo "$name rc=$rc"; tail -c 900 "$OUT/$name.out"; tail -3 "$OUT/$name.err"; if [ $rc -ne 0 ]; then exit $rc; fi; }
+run pytest 900 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread
+run smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
+run bench_default 300 python bench.py
+run bench_msa 400 python bench.py --algo msa --p 0.002 --batch-per-gpu 1000000 --steps 1 --warmup 1
+run bench_dna272 200 python bench.py --workload dna272
+exit 0
