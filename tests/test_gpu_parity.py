@@ -589,3 +589,4 @@ def test_host_lr_table_path(G, og, codewords, monkeypatch):
     ref_h, _, ref_it, ref_v = og.decode_batch(mixed, 60, algo=0, threads=8, want_post=False)
     h, _, it, v = G.decode(mixed, max_iter=60, post=None)
     assert np.array_equal(h, ref_h) and np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool))
+
