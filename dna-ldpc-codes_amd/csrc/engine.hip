@@ -928,7 +928,9 @@ int Engine::decode(const double* d_in, int in_kind, int64_t B, int32_t max_iter,
         }
         return LDPC_OK;
     }
-    if (xr) return run_xr(d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
+    // (the XCD-resident slots pack iteration counts in 16 bits; longer decodes
+    // take the engine's small tiled state)
+    if (xr && max_iter <= 0xffff) return run_xr(d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
     if (cont) return run_cont(d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
     // balanced passes of <= cap codewords (multiples of 64 except the tail)
     const int64_t npass = (B + cap - 1) / cap;

@@ -61,6 +61,7 @@ def test_xr_bitexact(gpu, og, codewords, xr, k):
     assert (it[150:] == 50).all() and not v[150:].any() and len(np.unique(it[:150])) > 2
     _cmp(G, og, llr[:70], 0)
     _cmp(G, og, llr[148:149], 50)
+    _cmp(G, og, llr[140:156], 70000) if k == 1 else None  # beyond the slots' 16-bit counts: the tiled state
     _cmp(G, og, llr[:5], 50)
     rng = np.random.default_rng(21)
     llr = synth.dna_like_llrs(codewords, seed=2, reads=60000)[:100]
