@@ -43,6 +43,39 @@ __global__ __launch_bounds__(256, 2) void rows_rmw(double* a, size_t nwaves, int
     }
 }
 
+// the same shapes with two codewords per lane (16 B per lane, 1024 B per
+// wave-segment): half the memory instructions per byte
+template <int SEG>
+__global__ __launch_bounds__(256, 2) void rows_rmw2(double2* a, size_t nwaves)
+{
+    const int lane = threadIdx.x & 63;
+    const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nwaves) return;
+    double2* s = a + w * SEG * 64 + lane;
+    double2 x[SEG];
+#pragma unroll
+    for (int k = 0; k < SEG; k++) x[k] = s[k * 64];
+#pragma unroll
+    for (int k = 0; k < SEG; k++) s[k * 64] = make_double2(x[k].x * 1.0000001 + 1e-300, x[k].y * 1.0000001 + 1e-300);
+}
+
+__global__ __launch_bounds__(256) void cols_rmw2(double2* a, const int* __restrict__ idx, size_t nwaves, size_t nseg)
+{
+    const int lane = threadIdx.x & 63;
+    const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nwaves) return;
+    const size_t tile = (w * 8) / nseg;
+    double2 v[8];
+    size_t o[8];
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        o[s] = ((size_t)idx[(w * 8 + s) % nseg] + tile * nseg) * 64 + lane;
+        v[s] = a[o[s]];
+    }
+#pragma unroll
+    for (int s = 0; s < 8; s++) a[o[s]] = make_double2(v[s].x * 1.5 + 1e-300, v[s].y * 1.5 + 1e-300);
+}
+
 // var shape: segment ids of one tile are a random permutation; wave w of a
 // tile takes 8 of them
 __global__ __launch_bounds__(256) void cols_rmw(double* a, const int* __restrict__ idx, size_t nwaves, size_t nseg,
@@ -96,6 +129,41 @@ int main(int argc, char** argv)
                 hipLaunchKernelGGL(rows_rmw<72>, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, 0, a, nw, 1);
             CK(hipDeviceSynchronize());
             std::printf("calib %.0f MB: %zu waves, %.0f bytes read + written per dispatch\n", mb, nw, (double)nw * 72 * 512);
+        }
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "wide") {
+        // one pass per launch, 8 B vs 16 B per lane, same bytes
+        std::printf("%8s %10s %10s %10s %10s\n", "MB", "rows72x8", "rows72x16", "cols8x8", "cols8x16");
+        for (double mb : {96.0, 128.0, 160.0, 192.0, 224.0, 256.0, 2048.0}) {
+            const size_t nseg_tot = (size_t)(mb * (1 << 20)) / 512;
+            double gbs[4];
+            for (int v = 0; v < 4; v++) {
+                const bool wide = v & 1, rows = v < 2;
+                const size_t segs = wide ? nseg_tot / 2 : nseg_tot;  // 1024 B segments when wide
+                const size_t nseg = segs < E ? segs : E;
+                const size_t nw = rows ? segs / 72 : (segs / nseg) * nseg / 8;
+                const double bytes = 2.0 * (double)nw * (rows ? 72 : 8) * (wide ? 1024 : 512);
+                const unsigned grid = (unsigned)((nw + 3) / 4);
+                auto go = [&]() {
+                    if (rows && !wide) hipLaunchKernelGGL(rows_rmw<72>, dim3(grid), dim3(256), 0, 0, a, nw, 1);
+                    else if (rows) hipLaunchKernelGGL(rows_rmw2<72>, dim3(grid), dim3(256), 0, 0, (double2*)a, nw);
+                    else if (!wide) hipLaunchKernelGGL(cols_rmw, dim3(grid), dim3(256), 0, 0, a, idx, nw, nseg, 1);
+                    else hipLaunchKernelGGL(cols_rmw2, dim3(grid), dim3(256), 0, 0, (double2*)a, idx, nw, nseg);
+                };
+                const int reps = 30;
+                go(); go();
+                CK(hipDeviceSynchronize());
+                CK(hipEventRecord(e0));
+                for (int r = 0; r < reps; r++) go();
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                gbs[v] = bytes * reps / (ms * 1e-3) / 1e9;
+            }
+            std::printf("%8.0f %10.1f %10.1f %10.1f %10.1f\n", mb, gbs[0], gbs[1], gbs[2], gbs[3]);
+            std::fflush(stdout);
         }
         return 0;
     }
