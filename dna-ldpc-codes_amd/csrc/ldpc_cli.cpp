@@ -3,7 +3,7 @@
 //
 //   ldpc <bSystematic> <decoder_type> <channel_type> <seed> <max_iter> <frame_num>
 //        [<target_frame_err> if frame_num == 0] <codeword_base> <soft_base> <pchk_base>
-//        <EbNo | eps (BEC) | p (BSC)> <punct> <short> <target> [<VN0> <VN1> if target]
+//        <EbNo | eps (BEC) | p (BSC)> <punct> <short> <target> [punct/short/target args]
 //
 // Argument parsing follows SetUp (DNA_main.cpp:300-505) for this subset;
 // decoder_type 0 = BP (dec.cpp:583), 20/21/22 = float min-sum (dec.cpp:1216,
@@ -15,6 +15,19 @@
 // (Print_All_Result, DNA_main.cpp:965-1123), stdout summary (Set_Code :551-556,
 // Print_One_Result :1170-1182).  The decode itself runs on the GPU through the
 // C ABI; there is no CPU decode path.
+//
+// Puncturing / shortening (SetUp :333-478, Set_Code :565-605, LDPC_Channel
+// :1375-1418): the argv and the side files (<pchk>.txt with the SC-code
+// multiplicities for types 2-4, <pchk>_punct.txt for type 5) are read as the
+// reference reads them; the code rate (and g_std_dev) and the result-file
+// lines follow.  On the AWGN / BSC channels the reference edits only the
+// received LR: punctured bits get LR = 1 (types 1, 2), shortened bits LR =
+// exp(30) (type 1, AWGN).  BP decodes from that LR, so this build passes LLR 0
+// / 30.0, whose host exp is the same LR bit for bit; min-sum and Gallager
+// read the unedited LLR / hard input, as in the reference.  Types 3-5 and BEC
+// erasure marks only change the hard input of the BEC decoders, which are
+// out of scope.  Indices outside the code, and shortening type 2 with an
+// SC-code length (undefined behaviour in the reference: LR[-1]), exit 1.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -75,9 +88,38 @@ int main(int argc, char** argv)
     const int punct = std::atoi(arg());
     const int shortening = std::atoi(arg());
     const int targeting = std::atoi(arg());
+    int p_start = 0, p_end = 0, p_start1 = 0, p_end1 = 0, p_start2 = 0, p_end2 = 0;
+    int s_start = 0, s_end = 0, s_etha = 0, s_num = 0, sc_w = 0, sc_L = 0;
+    std::vector<int> sc_M;  // g_SC_CODE_M (types 2-4)
     int target_VN[2] = {0, 0};
+    if (punct > 0 && punct != 5) { p_start = std::atoi(arg()); p_end = std::atoi(arg()); }
+    if (shortening == 1) { s_start = std::atoi(arg()); s_end = std::atoi(arg()); }
+    if (shortening == 2) { s_etha = std::atoi(arg()); s_num = std::atoi(arg()); }
     if (targeting) { target_VN[0] = std::atoi(arg()); target_VN[1] = std::atoi(arg()); }
-    if (punct != 0 || shortening != 0) die("ldpc: puncturing/shortening are not supported by this build");
+    auto read_ints = [&](const std::string& path, int n, std::vector<int>& out) {
+        std::vector<std::string> tok;
+        if (n > 0 && !read_tokens(path, tok, (size_t)n)) {
+            std::fprintf(stderr, "ldpc: cannot open %s\n", path.c_str());
+            std::exit(1);
+        }
+        // a short file leaves the calloc'd zeros, as fscanf does
+        for (int i = 0; i < n; i++) out.push_back(i < (int)tok.size() ? std::atoi(tok[(size_t)i].c_str()) : 0);
+    };
+    if (punct >= 2 && punct <= 4) {
+        // SetUp :355-431: [start1 end1 (type 4)] w L, <pchk>.txt holds D = L + w - 1
+        // multiplicities (and, for type 2, D more that only the SC decoders use)
+        if (punct == 4) { p_start1 = std::atoi(arg()); p_end1 = std::atoi(arg()); }
+        sc_w = std::atoi(arg());
+        sc_L = std::atoi(arg());
+        const int D = sc_L + sc_w - 1;
+        if (sc_L < 0 || D < 0 || (D < sc_L)) die("ldpc: SC-code w / L out of range");
+        read_ints(pchk_base + ".txt", D, sc_M);
+        if (punct >= 3) { p_start2 = std::atoi(arg()); p_end2 = std::atoi(arg()); }
+    }
+    if (punct == 5 && sc_L > 0) {  // SetUp :468-478 reads g_SC_CODE_L entries (0 outside SC runs)
+        std::vector<int> unused;
+        read_ints(pchk_base + "_punct.txt", sc_L, unused);
+    }
     if (argc != pos) { std::fprintf(stderr, "\n\nargc error!\n\n"); return 1; }
     int algo;
     // LDPC_Decode DNA_main.cpp:1565-1594.  The DNA build never sets
@@ -108,7 +150,24 @@ int main(int argc, char** argv)
     std::printf("g_CODE_M : %d\n", M);
     std::printf("\n");
     if (!targeting) { target_VN[0] = 1; target_VN[1] = N; }
-    const double rate = 1.0 - (double)M / (double)N;
+    double rate;  // Set_Code :565-605 (g_rand_type = RAND_SEED, g_save_type = 0 in this build)
+    if (punct == 1) {
+        const double np = (double)(p_end - p_start + 1);
+        rate = 1.0 - ((double)M - np) / ((double)N - np);
+    } else if (punct >= 2 && punct <= 4) {
+        int np = (p_end - p_start + 1) * sc_L;
+        if (punct >= 3) np += p_end2 - p_start2 + 1;
+        if (punct == 4) np += (p_end1 - p_start1 + 1) * (sc_w - 1);
+        rate = 1.0 - (double)(M - np) / (double)(N - np);
+    } else if (shortening == 1) {
+        rate = 1.0 - (double)M / (double)(N - (s_end - s_start + 1));
+    } else if (shortening == 2) {
+        if (s_etha == 0) die("ldpc: shortening type 2 needs a nonzero period");
+        const int ns = (int)(s_num * std::floor((double)sc_L / (double)s_etha));
+        rate = 1.0 - (double)M / (double)(N - ns);
+    } else {
+        rate = 1.0 - (double)M / (double)N;
+    }
     const double std_dev = 1 / std::sqrt(2 * rate * std::pow(10.0, EbNo * 0.1));  // getStd_dev channel.cpp:9-16
 
     time_t t_start, t_end;
@@ -137,13 +196,36 @@ int main(int argc, char** argv)
         if (codeword[(size_t)i] != temp) raw++;
     }
 
+    // ---- LDPC_Channel's LR edits (:1375-1441), seen by BP only ----
+    std::vector<double> llr_bp(llr);
+    auto set_lr = [&](long idx, double v) {
+        if (idx < 0 || idx >= N) die("ldpc: punctured / shortened bit outside the code");
+        llr_bp[(size_t)idx] = v;  // LR = exp(v): exp(30.0), exp(0) = 1
+    };
+    if (shortening == 1 && channel_type == 0)
+        for (int i = s_start; i <= s_end; i++) set_lr(i - 1, 30.0);
+    if (shortening == 2 && channel_type == 0 && sc_L > 0)
+        die("ldpc: shortening type 2 with an SC-code length indexes LR[-1] in the reference (undefined)");
+    if (channel_type == 0 || channel_type == 1) {
+        if (punct == 1) {
+            for (int i = p_start; i <= p_end; i++) set_lr(i - 1, 0.0);
+        } else if (punct == 2) {
+            long idx = 0;
+            for (int j = 0; j < sc_L; j++) {
+                for (int i = p_start; i <= p_end; i++) set_lr(idx + i - 1, 0.0);
+                idx += sc_M[(size_t)j];
+            }
+        }
+    }
+
     // ---- LDPC_Decode on the GPU ----
     std::vector<uint8_t> hard((size_t)N);
     int32_t iters = 0;
     uint8_t valid = 0;
     ldpc_opts o{};
     o.exp_on_host = 1;
-    if (ldpc_decode(g, llr.data(), 1, max_iter, algo, hard.data(), nullptr, &iters, &valid, &o) != LDPC_OK) {
+    const double* in = algo == LDPC_ALGO_BP ? llr_bp.data() : llr.data();
+    if (ldpc_decode(g, in, 1, max_iter, algo, hard.data(), nullptr, &iters, &valid, &o) != LDPC_OK) {
         std::fprintf(stderr, "ldpc: decode failed: %s\n", ldpc_last_error());
         return 1;
     }
@@ -225,6 +307,8 @@ int main(int argc, char** argv)
     std::fprintf(fr, "dc            : %d\n", dc);
     std::fprintf(fr, "bRegular_dc   : %d\n", rdc);
     if (targeting) std::fprintf(fr, "target_VN:%d~%d \n\n", target_VN[0], target_VN[1]);
+    if (punct) std::fprintf(fr, "[Type: %d] Punctuation_VN:%d~%d \n\n", punct, p_start, p_end);
+    if (shortening == 1) std::fprintf(fr, "[Type: %d] Shortening_VN:%d~%d \n\n", shortening, s_start, s_end);
     std::fprintf(fr, "=============================================\n");
     std::fprintf(fr, "                 result\n");
     std::fprintf(fr, "=============================================\n");

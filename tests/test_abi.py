@@ -126,6 +126,38 @@ def test_cli_rejects_bad_argc():
     assert r.returncode == 1 and "argc error!" in r.stderr
 
 
+def test_cli_punct_short_argv(tmp_path):
+    """Puncturing / shortening argv as SetUp consumes it (DNA_main.cpp:333-478):
+    counts per type, the SC-code side file of types 2-4, and the exits for
+    indices outside the code.  Every case stops before any GPU call."""
+    import shutil
+    exe = os.path.join(ROOT, "dna-ldpc-codes_amd", "bin", "ldpc")
+    d = str(tmp_path)
+    shutil.copyfile(PCHK, os.path.join(d, "code.pchk"))
+    for f in ("cw", "soft"):
+        with open(os.path.join(d, f + ".txt"), "w") as fh:
+            fh.write("0 " * 18432)
+    head = ["0", "0", "0", "7", "5", "1", "cw", "soft", "code", "0"]
+
+    def run(*tail):
+        return subprocess.run([exe, *head, *map(str, tail)], cwd=d, capture_output=True, text=True)
+
+    for tail in [(1, 0, 0), (1, 0, 0, 5), (0, 1, 0, 1), (0, 2, 0, 3), (2, 0, 0, 1, 2, 3), (0, 0, 1, 5)]:
+        r = run(*tail)  # one argument short of what SetUp reads
+        assert r.returncode == 1 and "argc error!" in r.stderr, tail
+    r = run(1, 0, 0, 1, 2, 99)  # one too many
+    assert r.returncode == 1 and "argc error!" in r.stderr
+    r = run(2, 0, 0, 1, 2, 3, 4)  # type 2 without <pchk>.txt
+    assert r.returncode == 1 and "cannot open" in r.stderr and "code.txt" in r.stderr
+    with open(os.path.join(d, "code.txt"), "w") as fh:
+        fh.write("18431\n")  # D = L + w - 1 = 4 entries; the missing ones read as 0
+    r = run(2, 0, 0, 1, 2, 3, 2)  # position 1 starts at bit 18431: 18432.. is outside
+    assert r.returncode == 1 and "outside the code" in r.stderr
+    for tail in [(1, 0, 0, 0, 3), (1, 0, 0, 18430, 18433), (0, 1, 0, 18432, 18433)]:
+        r = run(*tail)
+        assert r.returncode == 1 and "outside the code" in r.stderr, tail
+
+
 def test_graph_blocks_array_structure(L):
     """ldpc_graph_blocks: the DNA code is RS-LDPC(8, 72, 8) with permuted
     columns; its column blocks are found by row-set matching and equal the RS

@@ -109,3 +109,61 @@ def test_cli_other_decoder_types(tmp_path, og, codewords, dtype, algo):
     else:
         h, _, _, _ = og.decode_int_batch(llr[None, :], 30, algo)
     assert np.array_equal(dec, h[0])
+
+
+def _cli(d, dtype, cwb, soft, max_iter, tail, channel="0", param="0"):
+    argv = [EXE, "0", str(dtype), channel, "7", str(max_iter), "1", cwb, soft, "decode_n18432_m2048_final", param,
+            *map(str, tail)]
+    r = subprocess.run(argv, cwd=d, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return np.array(open(os.path.join(d, f"dec_{cwb}.txt")).read().split(), dtype=np.uint8)
+
+
+def test_cli_puncturing_shortening(tmp_path, og, codewords):
+    """LDPC_Channel (DNA_main.cpp:1375-1441): puncturing type 1 sets LR = 1
+    on bits start..end (AWGN and BSC), shortening type 1 sets LR = exp(30) (AWGN);
+    BP decodes the edited LR, min-sum the unedited LLR.  Type 2 punctures
+    start..end of every SC position, stepping by <pchk>.txt's multiplicities.
+    Result file: code rate of Set_Code (:574-597) and the type lines."""
+    d = str(tmp_path)
+    llr = synth.dna_like_llrs(codewords, seed=1, reads=58000)[20]
+    cwb, soft = _write_inputs(d, codewords[20], llr)
+
+    def ref(x, algo=0, it=60):
+        return og.decode_batch(x[None, :], it, algo=algo, threads=1, want_post=False)[0][0]
+
+    def edited(tail, x, **kw):
+        # max_iter 0 returns the initial decisions: the edit must show there
+        h0 = _cli(d, 0, cwb, soft, 0, tail, **kw)
+        assert np.array_equal(h0, ref(x, it=0)) and not np.array_equal(h0, ref(llr, it=0))
+        return _cli(d, 0, cwb, soft, 60, tail, **kw)
+
+    x = llr.copy()
+    x[99:400] = 0.0  # bits 100..400
+    assert np.array_equal(edited((1, 0, 0, 100, 400), x), ref(x))
+    res = os.path.join(d, f"result_({soft}.txt)_decode_n18432_m2048_final.pchk_0_0.000dB_0_60_7.txt")
+    txt = open(res).read()
+    assert "[Type: 1] Punctuation_VN:100~400 \n\n" in txt
+    assert "code rate     : %.3f\n" % (1.0 - (2048 - 301) / (18432 - 301)) in txt
+    assert np.array_equal(edited((1, 0, 0, 100, 400), x, channel="1", param="0.02"), ref(x))
+    # min-sum reads g_received_LLR, which puncturing leaves alone
+    assert np.array_equal(_cli(d, 20, cwb, soft, 60, (1, 0, 0, 100, 400)), ref(llr, algo=1))
+
+    x = llr.copy()
+    x[4999:5100] = 30.0
+    assert np.array_equal(edited((0, 1, 1, 5000, 5100, 1, 18432), x), ref(x))
+    txt = open(res).read()
+    assert "target_VN:1~18432 \n\n[Type: 1] Shortening_VN:5000~5100 \n\n" in txt
+    assert "code rate     : %.3f\n" % (1.0 - 2048 / (18432 - 101)) in txt
+    # BSC: the reference shortens only on AWGN / BEC
+    assert np.array_equal(_cli(d, 0, cwb, soft, 0, (0, 1, 0, 5000, 5100), channel="1", param="0.02"), ref(llr, it=0))
+
+    with open(os.path.join(d, "decode_n18432_m2048_final.txt"), "w") as f:
+        f.write("".join(f"{m}\n" for m in [256, 512, 1024, 7, 7]))  # M (w + L - 1 = 4 entries), then Mc
+    x = llr.copy()
+    for base in (0, 256, 768):  # L = 3 positions
+        x[base + 9:base + 20] = 0.0  # bits 10..20 of each
+    assert np.array_equal(edited((2, 0, 0, 10, 20, 2, 3), x), ref(x))
+    txt = open(res).read()
+    assert "[Type: 2] Punctuation_VN:10~20 \n\n" in txt
+    assert "code rate     : %.3f\n" % (1.0 - (2048 - 33) / (18432 - 33)) in txt
