@@ -1080,10 +1080,11 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     const int64_t tiles = std::min<int64_t>(cap_tiles, (B + 63) / 64);
     if (d_post && !post_t) LDPC_HIP(hipMalloc((void**)&post_t, (size_t)cap * N * sizeof(double)));
     double* pt = d_post ? post_t : nullptr;
-    LDPC_HIP(hipMemsetAsync(active, 0, (size_t)tiles * sizeof(uint64_t), stream));
-    LDPC_HIP(hipMemsetAsync(d_fresh, 0, (size_t)tiles * sizeof(uint64_t), stream));
-    LDPC_HIP(hipMemsetAsync(d_occ, 0, (size_t)tiles * sizeof(uint64_t), stream));
-    LDPC_HIP(hipMemsetAsync(d_ctr, 0, sizeof(unsigned long long), stream));
+    // lane masks, claim counter + occupancy ring, and (when allocated) the
+    // syndrome words, in one launch
+    static_assert(1 + kRing <= 256, "occupancy ring");
+    LAUNCH(K_OTHER, klaunch(k_cont_reset, dim3((unsigned)std::min<int64_t>((tiles + 255) / 256, 1024)), dim3(256), 0,
+                            stream, active, d_fresh, d_occ, d_ctr, 1 + kRing, d_unsat, d_done, tiles));
     ContState cs{active, d_fresh, d_occ, d_lane_b, d_lane_n, d_ctr, nullptr, B};
     ContOut co{d_hard, d_post, d_iters, d_valid, post_t, prior, msa, post_kind == LDPC_POST_RATIO ? 1 : 0};
     const Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0};
@@ -1113,8 +1114,6 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         // step and the lane bookkeeping, ResStep) then variable (+ the
         // finished codewords' outputs) over the whole pool, messages in place;
         // the occupancy is read every res_poll steps, kLag polls behind
-        LDPC_HIP(hipMemsetAsync(d_unsat, 0, (size_t)tiles * sizeof(unsigned long long), stream));
-        LDPC_HIP(hipMemsetAsync(d_done, 0, (size_t)tiles * sizeof(unsigned int), stream));
         ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, co};
         const Refill rfr{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
                          d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
@@ -1136,7 +1135,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                 const int64_t pi = s / every;
                 const int slot = (int)(pi % kRing);
                 rs.cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
-                if (poll) LDPC_HIP(hipMemsetAsync(rs.cs.occ_count, 0, sizeof(unsigned long long), stream));
+                rs.cs.occ_clear = poll ? d_ctr + 1 + (pi + 1) % kRing : nullptr;
                 for (int64_t t = 0; t < tiles && rc == LDPC_OK; t++)
                     rc = launch_pingpong(stream, t, (s == 0 && t == 0) ? -1 : (t + tiles - 1) % tiles, pt, rs, rfr);
                 if (rc) break;
@@ -1225,7 +1224,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             const int64_t pi = s / every;
             const int slot = (int)(pi % kRing);
             rs.cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
-            if (poll) LDPC_HIP(hipMemsetAsync(rs.cs.occ_count, 0, sizeof(unsigned long long), stream));
+            rs.cs.occ_clear = poll ? d_ctr + 1 + (pi + 1) % kRing : nullptr;
             if (res_syn_split > 0) {  // separate multi-block syndrome, then a plain in-place check
                 LAUNCH(K_SYN, klaunch(k_syndrome_split<72>, dim3((unsigned)res_syn_split, (unsigned)tiles),
                                                  dim3(256), 0, stream, M, rs));
@@ -1253,8 +1252,6 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     if (syn_fused) {
         // grouped steps with the syndrome fused into each group's check
         // launch (as the resident pool); polled every step, kLag behind
-        LDPC_HIP(hipMemsetAsync(d_unsat, 0, (size_t)tiles * sizeof(unsigned long long), stream));
-        LDPC_HIP(hipMemsetAsync(d_done, 0, (size_t)tiles * sizeof(unsigned int), stream));
         ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, co};
         const Refill rfr{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
                          d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
@@ -1264,7 +1261,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             if (s >= limit) return overrun(s);
             const int slot = (int)(s % kRing);
             rs.cs.occ_count = d_ctr + 1 + slot;
-            LDPC_HIP(hipMemsetAsync(rs.cs.occ_count, 0, sizeof(unsigned long long), stream));
+            rs.cs.occ_clear = d_ctr + 1 + (s + 1) % kRing;
             const int64_t gstep = low ? std::max(group_tiles, c2v_tiles) : group_tiles;
             for (int64_t t0 = 0; t0 < tiles; t0 += gstep) {
                 const unsigned gt = (unsigned)std::min<int64_t>(gstep, tiles - t0);
@@ -1295,17 +1292,14 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     const Refill rfs{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
                      d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
     const bool split = syn_split > 0 && reg_rowT && g->dc_max == 72;
-    if (split) {
-        LDPC_HIP(hipMemsetAsync(d_unsat, 0, (size_t)tiles * sizeof(unsigned long long), stream));
-        LDPC_HIP(hipMemsetAsync(d_done, 0, (size_t)tiles * sizeof(unsigned int), stream));
-    }
     const int64_t limit = step_limit(1);
     for (int64_t s = 0;; s++) {
         if (s >= limit) return overrun(s);
         const int slot = (int)(s % kRing);
         cs.occ_count = d_ctr + 1 + slot;
+        cs.occ_clear = d_ctr + 1 + (s + 1) % kRing;
         rss.cs.occ_count = cs.occ_count;
-        LDPC_HIP(hipMemsetAsync(cs.occ_count, 0, sizeof(unsigned long long), stream));
+        rss.cs.occ_clear = cs.occ_clear;
         if (split)
             LAUNCH(K_SYN, klaunch(k_syndrome_split<72>, dim3((unsigned)syn_split, (unsigned)tiles), dim3(256),
                                              0, stream, M, rss));

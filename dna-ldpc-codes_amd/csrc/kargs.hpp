@@ -35,6 +35,10 @@ struct ContState {
     unsigned long long* next_b;  // global claim counter
     unsigned long long* occ_count;  // occupied lanes after this step (host polls it)
     int64_t B;
+    // the next poll's counter, zeroed by tile 0's bookkeeping of this step (its
+    // previous D2H copy, kRing polls back, is stream-ordered before) instead
+    // of a memset launch per poll
+    unsigned long long* occ_clear = nullptr;
 };
 
 struct ContOut {

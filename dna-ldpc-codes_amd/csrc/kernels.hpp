@@ -159,6 +159,7 @@ __device__ __forceinline__ void cont_lanes(int64_t t, uint64_t occ, uint64_t U, 
             cs.occupied[t] = Cm | Fr;
             *s_fin = F;
             if ((Cm | Fr) && cs.occ_count) atomicAdd(cs.occ_count, (unsigned long long)__popcll(Cm | Fr));
+            if (t == 0 && cs.occ_clear) *cs.occ_clear = 0ull;
         }
     }
 }
@@ -690,12 +691,14 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
         // refills: the whole wave stores the prior line (live lanes their own
         // value) instead of a partial-line write by the refilled lanes alone
         if (CONT && frm != 0ull && ((full_lanes & 4) || fr)) prior[pj] = np;
-        if ((full_lanes & 1) || fr || live) {  // whole-line stores (others write 0, never read)
+        // whole-line stores (others write 0, never read) -- not in a tile that
+        // only hands out finished codewords (no live or refilled lane)
+        if (((full_lanes & 1) && touched) || fr || live) {
 #pragma unroll
             for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
         }
         const uint64_t m = __ballot(h);
-        if (lane == 0) {
+        if (lane == 0 && touched) {
             const size_t o = (size_t)t * N + j;
             const uint64_t old = (touched == ~0ull) ? 0ull : hard[o];
             hard[o] = (old & ~touched) | (m & touched);
@@ -1268,12 +1271,12 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
             if (post) post[pj] = L;
         }
         if (CONT && frm != 0ull && ((full_lanes & 4) || fr)) prior[pj] = np;
-        if ((full_lanes & 1) || fr || live) {
+        if (((full_lanes & 1) && touched) || fr || live) {  // as k_var_m
 #pragma unroll
             for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
         }
         const uint64_t m = __ballot(h);
-        if (lane == 0) {
+        if (lane == 0 && touched) {
             const size_t o = (size_t)t * N + j;
             const uint64_t old = (touched == ~0ull) ? 0ull : hard[o];
             hard[o] = (old & ~touched) | (m & touched);
@@ -1325,6 +1328,24 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ pos
 // Which lane decodes which codeword varies run to run; each codeword's
 // arithmetic does not.
 // ---------------------------------------------------------------------------
+// Start of a continuous decode: the lane masks, the claim counter, the
+// occupancy ring and the split syndrome's words in one launch (instead of a
+// memset launch each).
+__global__ __launch_bounds__(256) void k_cont_reset(uint64_t* __restrict__ active, uint64_t* __restrict__ fresh,
+                                                    uint64_t* __restrict__ occupied, unsigned long long* __restrict__ ctr,
+                                                    int32_t nctr, unsigned long long* __restrict__ unsat,
+                                                    unsigned* __restrict__ done, int64_t tiles)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tiles; i += (int64_t)gridDim.x * blockDim.x) {
+        active[i] = 0;
+        fresh[i] = 0;
+        occupied[i] = 0;
+        if (unsat) unsat[i] = 0;
+        if (done) done[i] = 0;
+    }
+    if (blockIdx.x == 0 && (int32_t)threadIdx.x < nctr) ctr[threadIdx.x] = 0;
+}
+
 // one block per tile
 template <int DC>
 __global__ __launch_bounds__(1024) void k_syndrome_cont(const uint64_t* __restrict__ hard,
