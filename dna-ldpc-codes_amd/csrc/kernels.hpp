@@ -367,16 +367,19 @@ __global__ __launch_bounds__(1024) void k_syndrome(const uint64_t* __restrict__ 
 // ---------------------------------------------------------------------------
 // c2v scratch: CSR order (row-contiguous) or CSC order (column-contiguous,
 // position pos[e]) so the variable phase reads each column contiguously
-template <int DC, bool NT, bool CSCL, bool INPLACE>
-__device__ __forceinline__ void check_bp_row(typename Msg<INPLACE>::in src, typename Msg<INPLACE>::out dst,
-                                             const int32_t* __restrict__ prow, int32_t row)
+template <int DC, bool NT, bool INPLACE>
+__device__ __forceinline__ void check_bp_load(double (&x)[DC], typename Msg<INPLACE>::in src)
+{
+#pragma unroll
+    for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
+}
+
+template <int DC, bool CSCL, bool INPLACE>
+__device__ __forceinline__ void check_bp_compute(const double (&x)[DC], typename Msg<INPLACE>::out dst,
+                                                 const int32_t* __restrict__ prow, int32_t row)
 {
     constexpr int SEG = 8;
     constexpr int NSEG = (DC + SEG - 1) / SEG;
-    double x[DC];
-#pragma unroll
-    for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
-
     double cp[NSEG];
     double p = 1.0;
 #pragma unroll
@@ -410,6 +413,15 @@ __device__ __forceinline__ void check_bp_row(typename Msg<INPLACE>::in src, type
     }
 }
 
+template <int DC, bool NT, bool CSCL, bool INPLACE>
+__device__ __forceinline__ void check_bp_row(typename Msg<INPLACE>::in src, typename Msg<INPLACE>::out dst,
+                                             const int32_t* __restrict__ prow, int32_t row)
+{
+    double x[DC];
+    check_bp_load<DC, NT, INPLACE>(x, src);
+    check_bp_compute<DC, CSCL, INPLACE>(x, dst, prow, row);
+}
+
 // SYN (resident pool, ResStep): the lanes run are the tile's occupied ones,
 // every wave also takes its row's parity over the previous variable phase's
 // ballots, and every block ends in res_arrive (no early exit).
@@ -430,22 +442,46 @@ __device__ __forceinline__ void check_bp_block(typename Msg<INPLACE>::in dmsg, t
     if constexpr (!SYN) {
         if (!run) return;
     }
-    uint64_t par = 0;
-    int32_t ln0 = 0;
-    int64_t b0 = 0;
-    if (SYN && act != 0) {
-        // the lane state for res_arrive's bookkeeping (used by the tile's last
-        // block only), loaded up front so it is not on the tail's chain
-        if (threadIdx.x < TILE && ((act >> lane) & 1ull)) {
-            ln0 = rs.cs.lane_n[t * TILE + lane];
-            b0 = rs.cs.lane_b[t * TILE + lane];
+    const auto src = dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
+    if constexpr (!SYN) {
+        check_bp_row<DC, NT, CSCL, INPLACE>(src, lr_t + lane, pos + (size_t)row * DC, row);
+    } else {
+        // Issue order inside one wave-uniform arm: the row's column indices,
+        // its DC message loads, the parity's ballot gathers (which need the
+        // indices), the arithmetic, then the XOR reduction -- the gathers'
+        // latency hides behind the messages instead of preceding them.  All
+        // lanes of an occupied tile run (whole-line stores whatever
+        // full_lanes says; unoccupied lanes' values are never read): a
+        // lane-masked arm, or a join between the loads and their uses, makes
+        // the compiler wait for every outstanding load there.
+        static_assert(DC <= 2 * TILE, "row parity: two gathers per lane");
+        const bool occ_l = (act >> lane) & 1ull;
+        // the lane state for res_arrive's bookkeeping (the tile's last block,
+        // on an occupied tile only), loaded up front off the tail's chain
+        const int32_t ln0 = rs.cs.lane_n[t * TILE + lane];
+        const int64_t b0 = rs.cs.lane_b[t * TILE + lane];
+        uint64_t par = 0;
+        if (row < M && act != 0) {
+            const int32_t* __restrict__ cols = rs.col_idx + (size_t)row * DC;
+            const int32_t c0 = cols[lane < DC ? lane : DC - 1];
+            const int32_t c1 = cols[TILE + lane < DC ? TILE + lane : DC - 1];
+            double x[DC];
+            check_bp_load<DC, NT, INPLACE>(x, src);
+            // opaque copies: the gather addresses (and the wait for the
+            // index loads) stay behind the message loads
+            int32_t d0 = c0, d1 = c1;
+            asm volatile("" : "+v"(d0), "+v"(d1));
+            const uint64_t* __restrict__ h = rs.hard + (size_t)t * rs.N;
+            const uint64_t g0 = h[d0];
+            const uint64_t g1 = h[d1];
+            check_bp_compute<DC, CSCL, INPLACE>(x, lr_t + lane, pos + (size_t)row * DC, row);
+            uint64_t p = (lane < DC ? g0 : 0ull) ^ (TILE + lane < DC ? g1 : 0ull);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) p ^= shfl_xor_u64(p, off);
+            par = p;
         }
-        if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
+        res_arrive(t, act, par, rs, occ_l ? ln0 : 0, occ_l ? b0 : 0, nrb);
     }
-    if (run)
-        check_bp_row<DC, NT, CSCL, INPLACE>(dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane, lr_t + lane,
-                                            pos + (size_t)row * DC, row);
-    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0, nrb);
 }
 
 template <int DC, bool NT, bool CSCL, bool SYN, bool INPLACE>
