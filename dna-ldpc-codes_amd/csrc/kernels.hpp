@@ -1100,8 +1100,12 @@ __device__ __forceinline__ void check_msa_c_row(const double* __restrict__ v2c, 
     for (int k = 0; k < DC; ++k) {
         const double a = __builtin_fabs(x[k]);
         negb[k / 32] |= ((x[k] >= 0) ? 0u : 1u) << (k % 32);
-        if (a < m1) { m2 = m1; m1 = a; i1 = k; }
-        else if (a < m2) m2 = a;
+        // if (a < m1) { m2 = m1; m1 = a; i1 = k; } else if (a < m2) m2 = a;
+        // as selects (no per-edge lane-masked branch); NaN compares false
+        const bool lt1 = a < m1, lt2 = a < m2;
+        m2 = lt1 ? m1 : (lt2 ? a : m2);
+        m1 = lt1 ? a : m1;
+        i1 = lt1 ? k : i1;
     }
     uint32_t neg = 0;
 #pragma unroll
