@@ -1065,9 +1065,10 @@ int Engine::run_xr(const double* d_in, int in_kind, int64_t B, int32_t max_iter,
 
 // Continuous batching over the whole batch: lanes are refilled as codewords
 // finish (kernels.hpp k_syndrome_cont), so a 64-codeword tile never idles on
-// its slowest member.  The host enqueues steps and stops kLag steps after
-// the device reports an empty pool (occupied lanes == 0 once the claim
-// counter has passed B); the few surplus steps find no occupied lane.
+// its slowest member.  The host enqueues steps and stops kLag (1 for a
+// single fill) steps after the device reports an empty pool (occupied lanes
+// == 0 once the claim counter has passed B); the few surplus steps find no
+// occupied lane.
 int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
                      int post_kind, int32_t* d_iters, uint8_t* d_valid)
 {
@@ -1090,6 +1091,10 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     const Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0};
     const bool reg_rowT = d_col_idx_T != nullptr;
     const int hard_vec = ((uintptr_t)d_hard % 8 == 0 && N % 8 == 0) ? 1 : 0;
+    // A batch that fits the lane pool in one fill (the DNA batch) polls one
+    // step behind instead of kLag: its steps take >= 30 us, time enough to
+    // enqueue the next, and the decode ends one empty step sooner.
+    const int lag = B <= tiles * 64 ? 1 : kLag;
     // Host step bound.  A lane finishes its codeword at most max_iter + 2
     // steps after claiming it (refill step, max_iter iterations, the final
     // syndrome), so within every window of max_iter + 2 steps each lane either
@@ -1101,7 +1106,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     const int64_t lanes = tiles * 64;
     const int64_t windows = (B + lanes - 1) / lanes + 1;
     auto step_limit = [&](int64_t every) {
-        return windows * ((int64_t)max_iter + 2) + (int64_t)(kLag + 2) * every + 8;
+        return windows * ((int64_t)max_iter + 2) + (int64_t)(lag + 2) * every + 8;
     };
     auto drained = [&](unsigned long long occ) { return occ == 0 && !debug_no_drain; };
     auto overrun = [&](int64_t steps) {
@@ -1144,8 +1149,8 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                                             hipMemcpyDeviceToHost, stream));
                     LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
                 }
-                if (poll && pi >= kLag) {
-                    const int old = (int)((pi - kLag) % kRing);
+                if (poll && pi >= lag) {
+                    const int old = (int)((pi - lag) % kRing);
                     LDPC_HIP(hipEventSynchronize(ev_ring[old]));
                     if (drained(h_occ[old])) break;
                 }
@@ -1195,8 +1200,8 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                     rc = launch_var(st, c2v + t * tsz, t, 1u, pt, rfr);
                 }
                 if (rc) break;
-                if (poll && pi >= kLag) {
-                    const int old = (int)((pi - kLag) % kRing);
+                if (poll && pi >= lag) {
+                    const int old = (int)((pi - lag) % kRing);
                     unsigned long long occ = 0;
                     for (int64_t t = 0; t < tiles; t++) {
                         LDPC_HIP(hipEventSynchronize(ev_tring[old][t]));
@@ -1241,8 +1246,8 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                 LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
             }
             if ((rc = launch_var(stream, c2v, 0, (unsigned)tiles, pt, rfr))) break;
-            if (poll && pi >= kLag) {
-                const int old = (int)((pi - kLag) % kRing);
+            if (poll && pi >= lag) {
+                const int old = (int)((pi - lag) % kRing);
                 LDPC_HIP(hipEventSynchronize(ev_ring[old]));
                 if (drained(h_occ[old])) break;
             }
@@ -1274,8 +1279,8 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             LDPC_HIP(hipMemcpyAsync(h_occ + slot, rs.cs.occ_count, sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                     stream));
             LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
-            if (s >= kLag) {
-                const int old = (int)((s - kLag) % kRing);
+            if (s >= lag) {
+                const int old = (int)((s - lag) % kRing);
                 LDPC_HIP(hipEventSynchronize(ev_ring[old]));
                 if (drained(h_occ[old])) break;
                 low = h_occ[old] * 32 < (unsigned long long)(tiles * 64);
@@ -1318,8 +1323,8 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             if ((rc = launch_check(stream, c2v, t0, gt))) return rc;
             if ((rc = launch_var(stream, c2v, t0, gt, pt, split ? rfs : rf))) return rc;
         }
-        if (s >= kLag) {
-            const int old = (int)((s - kLag) % kRing);
+        if (s >= lag) {
+            const int old = (int)((s - lag) % kRing);
             LDPC_HIP(hipEventSynchronize(ev_ring[old]));
             if (drained(h_occ[old])) break;
             low = h_occ[old] * 32 < (unsigned long long)(tiles * 64);
