@@ -1297,6 +1297,13 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     const Refill rfs{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
                      d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
     const bool split = syn_split > 0 && reg_rowT && g->dc_max == 72;
+    // single fill (the DNA batch): step 0's refill stores only the prior and
+    // step 1's check derives the first messages from it (k_check_bp_first),
+    // instead of writing and re-reading E copies per codeword
+    const bool first_fp = split && B <= tiles * 64 && algo == LDPC_ALGO_BP && !pipe && c2v != v2c &&
+                          env_int("LDPC_FIRST_FROM_PRIOR", 1) != 0;
+    Refill rfs0 = rfs;
+    rfs0.prior_only = first_fp ? 1 : 0;
     const int64_t limit = step_limit(1);
     for (int64_t s = 0;; s++) {
         if (s >= limit) return overrun(s);
@@ -1320,8 +1327,18 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         for (int64_t t0 = 0; t0 < tiles; t0 += gstep) {
             const unsigned gt = (unsigned)std::min<int64_t>(gstep, tiles - t0);
             int rc;
-            if ((rc = launch_check(stream, c2v, t0, gt))) return rc;
-            if ((rc = launch_var(stream, c2v, t0, gt, pt, split ? rfs : rf))) return rc;
+            if (first_fp && s == 1) {
+                const dim3 grid((M + 3) / 4, gt);
+                if (lr_csc)
+                    LAUNCH(K_CHECK, klaunch((k_check_bp_first<72, true>), grid, dim3(256), 0, stream, prior,
+                                            d_col_idx, c2v, active, d_csc_pos, M, N, (int64_t)g->E, t0, full_lanes));
+                else
+                    LAUNCH(K_CHECK, klaunch((k_check_bp_first<72, false>), grid, dim3(256), 0, stream, prior,
+                                            d_col_idx, c2v, active, d_csc_pos, M, N, (int64_t)g->E, t0, full_lanes));
+            } else if ((rc = launch_check(stream, c2v, t0, gt))) {
+                return rc;
+            }
+            if ((rc = launch_var(stream, c2v, t0, gt, pt, split ? (s == 0 ? rfs0 : rfs) : rf))) return rc;
         }
         if (s >= lag) {
             const int old = (int)((s - lag) % kRing);

@@ -24,6 +24,9 @@ struct Refill {
     double* post_out;       // [B][N] or nullptr
     int post_ratio;
     int hard_vec;           // hard_out is 8-byte aligned and N % 8 == 0: packed per-lane stores
+    // single fill (every lane refilled at once, none live): store only the
+    // prior; the next check derives d0 = 1 - 2/(1+LR) from it (k_check_bp_first)
+    int prior_only = 0;
 };
 
 struct ContState {

@@ -484,6 +484,35 @@ __device__ __forceinline__ void check_bp_block(typename Msg<INPLACE>::in dmsg, t
     }
 }
 
+// The first check of a single-fill decode (every occupied lane in its first
+// iteration; the refill stored only the prior, Refill::prior_only): each
+// edge's d0 = 1 - 2/(1+LR) of its column -- the expression and operands of
+// the refill (Init_Belief_Propagation dec.cpp:608-629 + the stored d of
+// dec.cpp:652) -- gathered from the tile's [N][64] prior instead of read from
+// E stored copies; then k_check_bp's arithmetic.  Same grid as k_check_bp.
+template <int DC, bool CSCL>
+__global__ __launch_bounds__(256, 2) void k_check_bp_first(const double* __restrict__ prior,
+                                                           const int32_t* __restrict__ col_idx,
+                                                           double* __restrict__ lr, const uint64_t* __restrict__ active,
+                                                           const int32_t* __restrict__ pos, int32_t M, int32_t N,
+                                                           int64_t E, int64_t t0, int full_lanes)
+{
+    const int lane = lane_id();
+    const int32_t row = (int32_t)blockIdx.x * 4 + wave_id();
+    const int64_t t = t0 + blockIdx.y;
+    const uint64_t act = active[t];
+    const bool run = row < M && ((full_lanes & 1) ? act != 0 : ((act >> lane) & 1ull));
+    if (!run) return;
+    const double* __restrict__ pt = prior + (size_t)t * N * TILE + lane;
+    const int32_t* __restrict__ cols = col_idx + (size_t)row * DC;
+    double x[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) x[k] = pt[(size_t)cols[k] * TILE];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) x[k] = 1.0 - 2.0 / (1.0 + x[k]);
+    check_bp_compute<DC, CSCL, false>(x, lr + (size_t)blockIdx.y * E * TILE + lane, pos + (size_t)row * DC, row);
+}
+
 template <int DC, bool NT, bool CSCL, bool SYN, bool INPLACE>
 __global__ __launch_bounds__(256, 2) void k_check_bp(typename Msg<INPLACE>::in dmsg, typename Msg<INPLACE>::out lr,
                                                      const uint64_t* __restrict__ active,
@@ -728,8 +757,10 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
         // value) instead of a partial-line write by the refilled lanes alone
         if (CONT && frm != 0ull && ((full_lanes & 4) || fr)) prior[pj] = np;
         // whole-line stores (others write 0, never read) -- not in a tile that
-        // only hands out finished codewords (no live or refilled lane)
-        if (((full_lanes & 1) && touched) || fr || live) {
+        // only hands out finished codewords (no live or refilled lane), nor
+        // for refills whose first check reads the prior (Refill::prior_only)
+        const bool skip_init = CONT && rf.prior_only && !live;
+        if (!skip_init && (((full_lanes & 1) && touched) || fr || live)) {
 #pragma unroll
             for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
         }

@@ -590,3 +590,45 @@ def test_host_lr_table_path(G, og, codewords, monkeypatch):
     h, _, it, v = G.decode(mixed, max_iter=60, post=None)
     assert np.array_equal(h, ref_h) and np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool))
 
+
+
+def test_single_fill_first_check_from_prior(gpu, G, og, codewords, monkeypatch):
+    """A batch that fits the lane pool in one fill (the DNA batch through
+    ldpc_decode): the refill stores only the prior and the first check takes
+    d0 = 1 - 2/(1+LR) from it (k_check_bp_first) instead of E stored copies.
+    Bit-exact against the oracle and identical to the stored-copies path
+    (LDPC_FIRST_FROM_PRIOR=0) at max_iter 0 / 1 / 2 / 60, with NaN / +-inf
+    inputs, for host LR (ldpc_decode) and device exp (Engine, LLR input)."""
+    rng = np.random.default_rng(33)
+    nasty = synth.dna_like_llrs(codewords, seed=6, reads=57000)[:150]
+    nasty[rng.random(nasty.shape) < 0.002] = np.nan
+    nasty[rng.random(nasty.shape) < 0.002] = np.inf
+    nasty[rng.random(nasty.shape) < 0.002] = -np.inf
+    cases = [(synth.dna_like_llrs(codewords, seed=7, reads=58000), it) for it in (0, 1, 2, 60)]
+    cases.append((nasty, 40))
+    for llr, it in cases:
+        ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, it, algo=0, post_mode=1, threads=8)
+        outs = []
+        for fp in ("1", "0"):
+            monkeypatch.setenv("LDPC_FIRST_FROM_PRIOR", fp)
+            h, p, i, v = G.decode(llr, max_iter=it, post="ratio")
+            assert np.array_equal(i, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
+            nan = np.isnan(ref_p)
+            assert np.array_equal(np.isnan(p), nan)
+            assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64))
+            outs.append((h, i))
+        assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    monkeypatch.delenv("LDPC_FIRST_FROM_PRIOR")
+    # device-resident engine, LLR input (device exp in the refill), one fill of 150
+    L = gpu
+    llr = synth.dna_like_llrs(codewords, seed=8, reads=58000)[:150]
+    B, N = llr.shape
+    eng = L.Engine(G, 0, "bp", chunk=B)
+    d_in = L.DeviceBuffer(0, B * N * 8)
+    d_in.upload(np.ascontiguousarray(llr))
+    d_h, d_i, d_v = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
+    eng.decode(d_in.at(0), L.IN_LLR, B, 100, d_h.at(0), None, L.POST_LLR, d_i.at(0), d_v.at(0))
+    eng.sync()
+    ref_h, _, ref_it, ref_v = og.decode_batch(llr, 100, algo=0, threads=8, want_post=False)
+    assert np.array_equal(d_i.download(np.empty(B, np.int32)), ref_it)
+    assert np.array_equal(d_h.download(np.empty((B, N), np.uint8)), ref_h)
