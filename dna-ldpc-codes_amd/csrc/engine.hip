@@ -108,10 +108,6 @@ Engine::~Engine()
     for (auto e : ev_pool) hipEventDestroy(e);
     hipFree(d_csc_pos);
     hipFree(d_fresh); hipFree(d_occ); hipFree(d_lane_b); hipFree(d_lane_n); hipFree(d_ctr);
-    if (poll_stream) { hipStreamSynchronize(poll_stream); hipStreamDestroy(poll_stream); }
-    for (int i = 0; i < kRing; i++)
-        if (ev_poll[i]) hipEventDestroy(ev_poll[i]);
-    if (ev_poll_join) hipEventDestroy(ev_poll_join);
     if (h_occ) hipHostFree(h_occ);
     for (int t = 0; t < kMaxTileStreams; t++) {
         if (tstream[t]) { hipStreamSynchronize(tstream[t]); hipStreamDestroy(tstream[t]); }
@@ -269,9 +265,6 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         LDPC_HIP(hipMalloc((void**)&d_ctr, (size_t)(1 + kRing) * sizeof(unsigned long long)));
         LDPC_HIP(hipHostMalloc((void**)&h_occ, (size_t)kRing * sizeof(unsigned long long), hipHostMallocDefault));
         for (int i = 0; i < kRing; i++) LDPC_HIP(hipEventCreateWithFlags(&ev_ring[i], hipEventDisableTiming));
-        LDPC_HIP(hipStreamCreateWithFlags(&poll_stream, hipStreamNonBlocking));
-        for (int i = 0; i < kRing; i++) LDPC_HIP(hipEventCreateWithFlags(&ev_poll[i], hipEventDisableTiming));
-        LDPC_HIP(hipEventCreateWithFlags(&ev_poll_join, hipEventDisableTiming));
         if (tile_streams) {
             for (int t = 0; t < kMaxTileStreams; t++) {
                 LDPC_HIP(hipStreamCreateWithFlags(&tstream[t], hipStreamNonBlocking));
@@ -1076,27 +1069,8 @@ int Engine::run_xr(const double* d_in, int in_kind, int64_t B, int32_t max_iter,
 // single fill) steps after the device reports an empty pool (occupied lanes
 // == 0 once the claim counter has passed B); the few surplus steps find no
 // occupied lane.
-int Engine::poll_copy(int slot, const unsigned long long* src)
-{
-    LDPC_HIP(hipEventRecord(ev_poll[slot], stream));
-    LDPC_HIP(hipStreamWaitEvent(poll_stream, ev_poll[slot], 0));
-    LDPC_HIP(hipMemcpyAsync(h_occ + slot, src, sizeof(unsigned long long), hipMemcpyDeviceToHost, poll_stream));
-    LDPC_HIP(hipEventRecord(ev_ring[slot], poll_stream));
-    return LDPC_OK;
-}
-
 int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
                      int post_kind, int32_t* d_iters, uint8_t* d_valid)
-{
-    const int rc = run_cont_steps(d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
-    // later work on the decode stream (and its syncs) sees the last poll copies
-    LDPC_HIP(hipEventRecord(ev_poll_join, poll_stream));
-    LDPC_HIP(hipStreamWaitEvent(stream, ev_poll_join, 0));
-    return rc;
-}
-
-int Engine::run_cont_steps(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard,
-                           double* d_post, int post_kind, int32_t* d_iters, uint8_t* d_valid)
 {
     using namespace dev;
     const int msa = algo == LDPC_ALGO_MSA;
@@ -1171,7 +1145,9 @@ int Engine::run_cont_steps(const double* d_in, int in_kind, int64_t B, int32_t m
                     rc = launch_pingpong(stream, t, (s == 0 && t == 0) ? -1 : (t + tiles - 1) % tiles, pt, rs, rfr);
                 if (rc) break;
                 if (poll) {
-                    if (int r = poll_copy(slot, rs.cs.occ_count)) return r;
+                    LDPC_HIP(hipMemcpyAsync(h_occ + slot, rs.cs.occ_count, sizeof(unsigned long long),
+                                            hipMemcpyDeviceToHost, stream));
+                    LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
                 }
                 if (poll && pi >= lag) {
                     const int old = (int)((pi - lag) % kRing);
@@ -1265,7 +1241,9 @@ int Engine::run_cont_steps(const double* d_in, int in_kind, int64_t B, int32_t m
             }
             if (rc) break;
             if (poll) {
-                if ((rc = poll_copy(slot, rs.cs.occ_count))) break;
+                LDPC_HIP(hipMemcpyAsync(h_occ + slot, rs.cs.occ_count, sizeof(unsigned long long),
+                                        hipMemcpyDeviceToHost, stream));
+                LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
             }
             if ((rc = launch_var(stream, c2v, 0, (unsigned)tiles, pt, rfr))) break;
             if (poll && pi >= lag) {
@@ -1298,7 +1276,9 @@ int Engine::run_cont_steps(const double* d_in, int in_kind, int64_t B, int32_t m
                 if (rc) return rc;
                 if ((rc = launch_var(stream, c2v, t0, gt, pt, rfr))) return rc;
             }
-            if (int r = poll_copy(slot, rs.cs.occ_count)) return r;
+            LDPC_HIP(hipMemcpyAsync(h_occ + slot, rs.cs.occ_count, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                    stream));
+            LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
             if (s >= lag) {
                 const int old = (int)((s - lag) % kRing);
                 LDPC_HIP(hipEventSynchronize(ev_ring[old]));
@@ -1341,7 +1321,8 @@ int Engine::run_cont_steps(const double* d_in, int in_kind, int64_t B, int32_t m
         else
             LAUNCH(K_SYN, klaunch(k_syndrome_cont<0>, dim3((unsigned)tiles), dim3(1024), 0, stream, hard,
                                              d_row_ptr, d_col_idx, d_col_idx_T, M, N, max_iter, cs, co));
-        if (int r = poll_copy(slot, cs.occ_count)) return r;
+        LDPC_HIP(hipMemcpyAsync(h_occ + slot, cs.occ_count, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+        LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
         const int64_t gstep = low ? std::max(group_tiles, c2v_tiles) : group_tiles;
         for (int64_t t0 = 0; t0 < tiles; t0 += gstep) {
             const unsigned gt = (unsigned)std::min<int64_t>(gstep, tiles - t0);

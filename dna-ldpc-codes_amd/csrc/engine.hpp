@@ -75,12 +75,6 @@ struct Engine {
     unsigned long long* d_ctr = nullptr;  // [0] claim counter, [1..kRing] occupancy ring
     unsigned long long* h_occ = nullptr;  // pinned mirror of the occupancy ring
     hipEvent_t ev_ring[kRing] = {};
-    // the occupancy copies run on their own stream, ordered after the step's
-    // bookkeeping by ev_poll, so the D2H blit is off the decode stream
-    hipStream_t poll_stream = nullptr;
-    hipEvent_t ev_poll[kRing] = {};
-    hipEvent_t ev_poll_join = nullptr;
-    int poll_copy(int slot, const unsigned long long* src);
     int32_t* d_csc_pos = nullptr;  // [E] CSC position of CSR edge e
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_chk[2] = {nullptr, nullptr}, ev_var[2] = {nullptr, nullptr}, ev_join = nullptr;
@@ -141,8 +135,6 @@ struct Engine {
     int init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, int64_t group = -1, int nt = -1,
              int pipelined = -1, int csc = -1, int cont_mode = -1, int res_mode = -1);
     int run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
-                 int post_kind, int32_t* d_iters, uint8_t* d_valid);
-        int run_cont_steps(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
                  int post_kind, int32_t* d_iters, uint8_t* d_valid);
     // decode Bc <= cap codewords whose [Bc][N] input is at d_in (device)
     int run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_iter, uint8_t* d_hard, double* d_post,
