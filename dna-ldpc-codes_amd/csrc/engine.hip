@@ -17,20 +17,20 @@
 // Stopped codewords are masked out of every later kernel (their state stays
 // frozen, exactly as the reference stops touching it), and a tile whose 64
 // codewords have all stopped costs one scalar load per wave.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "engine.hpp"
 #include "kernels.hpp"
 #include "kernels_int.hpp"
 #include "kernels_xr.hpp"
-#include <hip/hip_ext.h>
-
-#include <cstdlib>
 
 namespace ldpc {
 
@@ -109,6 +109,7 @@ Engine::~Engine()
     hipFree(d_csc_pos);
     hipFree(d_fresh); hipFree(d_occ); hipFree(d_lane_b); hipFree(d_lane_n); hipFree(d_ctr);
     if (h_occ) hipHostFree(h_occ);
+    if (h_poll) hipHostFree(h_poll);
     for (int t = 0; t < kMaxTileStreams; t++) {
         if (tstream[t]) { hipStreamSynchronize(tstream[t]); hipStreamDestroy(tstream[t]); }
         if (ev_tjoin[t]) hipEventDestroy(ev_tjoin[t]);
@@ -264,6 +265,10 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         LDPC_HIP(hipMalloc((void**)&d_lane_n, (size_t)cap * sizeof(int32_t)));
         LDPC_HIP(hipMalloc((void**)&d_ctr, (size_t)(1 + kRing) * sizeof(unsigned long long)));
         LDPC_HIP(hipHostMalloc((void**)&h_occ, (size_t)kRing * sizeof(unsigned long long), hipHostMallocDefault));
+        LDPC_HIP(hipHostMalloc((void**)&h_poll, (size_t)kRing * sizeof(unsigned long long),
+                               hipHostMallocCoherent | hipHostMallocMapped));
+        std::memset(h_poll, 0, (size_t)kRing * sizeof(unsigned long long));
+        LDPC_HIP(hipHostGetDevicePointer((void**)&d_poll, h_poll, 0));
         for (int i = 0; i < kRing; i++) LDPC_HIP(hipEventCreateWithFlags(&ev_ring[i], hipEventDisableTiming));
         if (tile_streams) {
             for (int t = 0; t < kMaxTileStreams; t++) {
@@ -1063,6 +1068,48 @@ int Engine::run_xr(const double* d_in, int in_kind, int64_t B, int32_t max_iter,
     return LDPC_OK;
 }
 
+void Engine::poll_arm(dev::ContState& cs, uint64_t q) const
+{
+    cs.occ_count = d_ctr + 1 + (q % kRing);
+    cs.occ_clear = d_ctr + 1 + ((q + 1) % kRing);
+    cs.poll_host = d_poll + (q % kRing);
+    cs.poll_tag = (q + 1) & ((1ull << (64 - dev::kOccTileShift)) - 1ull);  // never the initial 0
+}
+
+// Wait for poll q's device-written word.  The engine-wide sequence keeps tags
+// unique across decodes (a previous decode's trailing steps may still write
+// their slots).  The stream is queried while waiting: a device error, or a
+// stream that finished without the word, is an error instead of a hang.
+int Engine::poll_wait(uint64_t q, unsigned long long* occ)
+{
+    const unsigned long long want = (q + 1) & ((1ull << (64 - dev::kOccTileShift)) - 1ull);
+    volatile unsigned long long* w = h_poll + (q % kRing);
+    for (uint64_t spin = 1;; spin++) {
+        const unsigned long long v = *w;
+        if ((v >> dev::kOccTileShift) == want) {
+            *occ = v & dev::kOccMask;
+            return LDPC_OK;
+        }
+        if (spin % 64 == 0) {
+            const hipError_t e = hipStreamQuery(stream);
+            if (e == hipSuccess) {
+                const unsigned long long v2 = *w;
+                if ((v2 >> dev::kOccTileShift) == want) {
+                    *occ = v2 & dev::kOccMask;
+                    return LDPC_OK;
+                }
+                set_error("occupancy poll " + std::to_string(q) + ": the step finished without its device write");
+                return LDPC_ERR_DEVICE;
+            }
+            if (e != hipErrorNotReady) {
+                set_error(std::string("occupancy poll: ") + hipGetErrorString(e));
+                return LDPC_ERR_DEVICE;
+            }
+            std::this_thread::yield();
+        }
+    }
+}
+
 // Continuous batching over the whole batch: lanes are refilled as codewords
 // finish (kernels.hpp k_syndrome_cont), so a 64-codeword tile never idles on
 // its slowest member.  The host enqueues steps and stops kLag (1 for a
@@ -1087,6 +1134,8 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     LAUNCH(K_OTHER, klaunch(k_cont_reset, dim3((unsigned)std::min<int64_t>((tiles + 255) / 256, 1024)), dim3(256), 0,
                             stream, active, d_fresh, d_occ, d_ctr, 1 + kRing, d_unsat, d_done, tiles));
     ContState cs{active, d_fresh, d_occ, d_lane_b, d_lane_n, d_ctr, nullptr, B};
+    cs.ntiles = tiles;
+    const uint64_t q0 = poll_seq;  // this decode's first poll
     ContOut co{d_hard, d_post, d_iters, d_valid, post_t, prior, msa, post_kind == LDPC_POST_RATIO ? 1 : 0};
     const Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0};
     const bool reg_rowT = d_col_idx_T != nullptr;
@@ -1137,22 +1186,16 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             for (int64_t s = 0; rc == LDPC_OK; s++) {
                 if (s >= limit) { rc = overrun(s); break; }
                 const bool poll = (s % every) == every - 1;
-                const int64_t pi = s / every;
-                const int slot = (int)(pi % kRing);
-                rs.cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
-                rs.cs.occ_clear = poll ? d_ctr + 1 + (pi + 1) % kRing : nullptr;
+                const uint64_t q = poll ? poll_seq++ : 0;
+                if (poll) poll_arm(rs.cs, q);
+                else rs.cs.occ_count = rs.cs.occ_clear = rs.cs.poll_host = nullptr;
                 for (int64_t t = 0; t < tiles && rc == LDPC_OK; t++)
                     rc = launch_pingpong(stream, t, (s == 0 && t == 0) ? -1 : (t + tiles - 1) % tiles, pt, rs, rfr);
                 if (rc) break;
-                if (poll) {
-                    LDPC_HIP(hipMemcpyAsync(h_occ + slot, rs.cs.occ_count, sizeof(unsigned long long),
-                                            hipMemcpyDeviceToHost, stream));
-                    LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
-                }
-                if (poll && pi >= lag) {
-                    const int old = (int)((pi - lag) % kRing);
-                    LDPC_HIP(hipEventSynchronize(ev_ring[old]));
-                    if (drained(h_occ[old])) break;
+                if (poll && q >= q0 + (uint64_t)lag) {
+                    unsigned long long occ = 0;
+                    if ((rc = poll_wait(q - lag, &occ))) break;
+                    if (drained(occ)) break;
                 }
             }
             return rc;
@@ -1205,7 +1248,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                     unsigned long long occ = 0;
                     for (int64_t t = 0; t < tiles; t++) {
                         LDPC_HIP(hipEventSynchronize(ev_tring[old][t]));
-                        occ += h_occ_t[(size_t)old * kMaxTileStreams + t];
+                        occ += h_occ_t[(size_t)old * kMaxTileStreams + t] & dev::kOccMask;
                     }
                     if (drained(occ)) break;
                 }
@@ -1226,10 +1269,9 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         for (int64_t s = 0; rc == LDPC_OK; s++) {
             if (s >= limit) { rc = overrun(s); break; }
             const bool poll = (s % every) == every - 1;
-            const int64_t pi = s / every;
-            const int slot = (int)(pi % kRing);
-            rs.cs.occ_count = poll ? d_ctr + 1 + slot : nullptr;
-            rs.cs.occ_clear = poll ? d_ctr + 1 + (pi + 1) % kRing : nullptr;
+            const uint64_t q = poll ? poll_seq++ : 0;
+            if (poll) poll_arm(rs.cs, q);
+            else rs.cs.occ_count = rs.cs.occ_clear = rs.cs.poll_host = nullptr;
             if (res_syn_split > 0) {  // separate multi-block syndrome, then a plain in-place check
                 LAUNCH(K_SYN, klaunch(k_syndrome_split<72>, dim3((unsigned)res_syn_split, (unsigned)tiles),
                                                  dim3(256), 0, stream, M, rs));
@@ -1240,16 +1282,11 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                 rstep = nullptr;
             }
             if (rc) break;
-            if (poll) {
-                LDPC_HIP(hipMemcpyAsync(h_occ + slot, rs.cs.occ_count, sizeof(unsigned long long),
-                                        hipMemcpyDeviceToHost, stream));
-                LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
-            }
             if ((rc = launch_var(stream, c2v, 0, (unsigned)tiles, pt, rfr))) break;
-            if (poll && pi >= lag) {
-                const int old = (int)((pi - lag) % kRing);
-                LDPC_HIP(hipEventSynchronize(ev_ring[old]));
-                if (drained(h_occ[old])) break;
+            if (poll && q >= q0 + (uint64_t)lag) {
+                unsigned long long occ = 0;
+                if ((rc = poll_wait(q - lag, &occ))) break;
+                if (drained(occ)) break;
             }
         }
         return rc;
@@ -1264,9 +1301,8 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         const int64_t limit = step_limit(1);
         for (int64_t s = 0;; s++) {
             if (s >= limit) return overrun(s);
-            const int slot = (int)(s % kRing);
-            rs.cs.occ_count = d_ctr + 1 + slot;
-            rs.cs.occ_clear = d_ctr + 1 + (s + 1) % kRing;
+            const uint64_t q = poll_seq++;
+            poll_arm(rs.cs, q);
             const int64_t gstep = low ? std::max(group_tiles, c2v_tiles) : group_tiles;
             for (int64_t t0 = 0; t0 < tiles; t0 += gstep) {
                 const unsigned gt = (unsigned)std::min<int64_t>(gstep, tiles - t0);
@@ -1276,14 +1312,11 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                 if (rc) return rc;
                 if ((rc = launch_var(stream, c2v, t0, gt, pt, rfr))) return rc;
             }
-            LDPC_HIP(hipMemcpyAsync(h_occ + slot, rs.cs.occ_count, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                    stream));
-            LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
-            if (s >= lag) {
-                const int old = (int)((s - lag) % kRing);
-                LDPC_HIP(hipEventSynchronize(ev_ring[old]));
-                if (drained(h_occ[old])) break;
-                low = h_occ[old] * 32 < (unsigned long long)(tiles * 64);
+            if (q >= q0 + (uint64_t)lag) {
+                unsigned long long occ = 0;
+                if (int r = poll_wait(q - lag, &occ)) return r;
+                if (drained(occ)) break;
+                low = occ * 32 < (unsigned long long)(tiles * 64);
             }
         }
         return LDPC_OK;
@@ -1307,11 +1340,9 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     const int64_t limit = step_limit(1);
     for (int64_t s = 0;; s++) {
         if (s >= limit) return overrun(s);
-        const int slot = (int)(s % kRing);
-        cs.occ_count = d_ctr + 1 + slot;
-        cs.occ_clear = d_ctr + 1 + (s + 1) % kRing;
-        rss.cs.occ_count = cs.occ_count;
-        rss.cs.occ_clear = cs.occ_clear;
+        const uint64_t q = poll_seq++;
+        poll_arm(cs, q);
+        poll_arm(rss.cs, q);
         if (split)
             LAUNCH(K_SYN, klaunch(k_syndrome_split<72>, dim3((unsigned)syn_split, (unsigned)tiles), dim3(256),
                                              0, stream, M, rss));
@@ -1321,8 +1352,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         else
             LAUNCH(K_SYN, klaunch(k_syndrome_cont<0>, dim3((unsigned)tiles), dim3(1024), 0, stream, hard,
                                              d_row_ptr, d_col_idx, d_col_idx_T, M, N, max_iter, cs, co));
-        LDPC_HIP(hipMemcpyAsync(h_occ + slot, cs.occ_count, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
-        LDPC_HIP(hipEventRecord(ev_ring[slot], stream));
+
         const int64_t gstep = low ? std::max(group_tiles, c2v_tiles) : group_tiles;
         for (int64_t t0 = 0; t0 < tiles; t0 += gstep) {
             const unsigned gt = (unsigned)std::min<int64_t>(gstep, tiles - t0);
@@ -1340,11 +1370,11 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             }
             if ((rc = launch_var(stream, c2v, t0, gt, pt, split ? (s == 0 ? rfs0 : rfs) : rf))) return rc;
         }
-        if (s >= lag) {
-            const int old = (int)((s - lag) % kRing);
-            LDPC_HIP(hipEventSynchronize(ev_ring[old]));
-            if (drained(h_occ[old])) break;
-            low = h_occ[old] * 32 < (unsigned long long)(tiles * 64);
+        if (q >= q0 + (uint64_t)lag) {
+            unsigned long long occ = 0;
+            if (int r = poll_wait(q - lag, &occ)) return r;
+            if (drained(occ)) break;
+            low = occ * 32 < (unsigned long long)(tiles * 64);
         }
     }
     return LDPC_OK;

@@ -42,7 +42,16 @@ struct ContState {
     // previous D2H copy, kRing polls back, is stream-ordered before) instead
     // of a memset launch per poll
     unsigned long long* occ_clear = nullptr;
+    // occ_count packs (tiles counted) << kOccTileShift | occupied lanes; the
+    // last of ntiles tiles to count writes poll_tag << kOccTileShift |
+    // occupied lanes to poll_host (pinned host memory, system scope), which
+    // the host waits on instead of a D2H copy + event per poll
+    unsigned long long* poll_host = nullptr;
+    unsigned long long poll_tag = 0;
+    int64_t ntiles = 0;
 };
+constexpr int kOccTileShift = 40;
+constexpr unsigned long long kOccMask = (1ull << kOccTileShift) - 1ull;
 
 struct ContOut {
     uint8_t* hard;    // [B][N]

@@ -158,7 +158,13 @@ __device__ __forceinline__ void cont_lanes(int64_t t, uint64_t occ, uint64_t U, 
             cs.fresh[t] = Fr;
             cs.occupied[t] = Cm | Fr;
             *s_fin = F;
-            if ((Cm | Fr) && cs.occ_count) atomicAdd(cs.occ_count, (unsigned long long)__popcll(Cm | Fr));
+            if (cs.occ_count) {
+                const unsigned long long add = (1ull << kOccTileShift) | (unsigned long long)__popcll(Cm | Fr);
+                const unsigned long long old = atomicAdd(cs.occ_count, add);
+                if (cs.poll_host && (int64_t)(old >> kOccTileShift) + 1 == cs.ntiles)
+                    __hip_atomic_store(cs.poll_host, (cs.poll_tag << kOccTileShift) | ((old + add) & kOccMask),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             if (t == 0 && cs.occ_clear) *cs.occ_clear = 0ull;
         }
     }
