@@ -108,7 +108,6 @@ Engine::~Engine()
     for (auto e : ev_pool) hipEventDestroy(e);
     hipFree(d_csc_pos);
     hipFree(d_fresh); hipFree(d_occ); hipFree(d_lane_b); hipFree(d_lane_n); hipFree(d_ctr);
-    if (h_occ) hipHostFree(h_occ);
     if (h_poll) hipHostFree(h_poll);
     for (int t = 0; t < kMaxTileStreams; t++) {
         if (tstream[t]) { hipStreamSynchronize(tstream[t]); hipStreamDestroy(tstream[t]); }
@@ -118,8 +117,6 @@ Engine::~Engine()
     }
     if (h_occ_t) hipHostFree(h_occ_t);
     hipFree(d_occ_t);
-    for (int i = 0; i < kRing; i++)
-        if (ev_ring[i]) hipEventDestroy(ev_ring[i]);
     hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge); hipFree(d_col_row);
     hipFree(d_unsat); hipFree(d_done); hipFree(d_fin); hipFree(d_fin_b); hipFree(d_fin_n);
     hipFree(v2c); if (c2v != v2c) hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
@@ -264,12 +261,10 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         LDPC_HIP(hipMalloc((void**)&d_lane_b, (size_t)cap * sizeof(int64_t)));
         LDPC_HIP(hipMalloc((void**)&d_lane_n, (size_t)cap * sizeof(int32_t)));
         LDPC_HIP(hipMalloc((void**)&d_ctr, (size_t)(1 + kRing) * sizeof(unsigned long long)));
-        LDPC_HIP(hipHostMalloc((void**)&h_occ, (size_t)kRing * sizeof(unsigned long long), hipHostMallocDefault));
         LDPC_HIP(hipHostMalloc((void**)&h_poll, (size_t)kRing * sizeof(unsigned long long),
                                hipHostMallocCoherent | hipHostMallocMapped));
         std::memset(h_poll, 0, (size_t)kRing * sizeof(unsigned long long));
         LDPC_HIP(hipHostGetDevicePointer((void**)&d_poll, h_poll, 0));
-        for (int i = 0; i < kRing; i++) LDPC_HIP(hipEventCreateWithFlags(&ev_ring[i], hipEventDisableTiming));
         if (tile_streams) {
             for (int t = 0; t < kMaxTileStreams; t++) {
                 LDPC_HIP(hipStreamCreateWithFlags(&tstream[t], hipStreamNonBlocking));

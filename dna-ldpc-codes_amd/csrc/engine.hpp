@@ -73,8 +73,6 @@ struct Engine {
     int64_t* d_lane_b = nullptr;
     int32_t* d_lane_n = nullptr;
     unsigned long long* d_ctr = nullptr;  // [0] claim counter, [1..kRing] occupancy ring
-    unsigned long long* h_occ = nullptr;  // pinned mirror of the occupancy ring (tile streams)
-    hipEvent_t ev_ring[kRing] = {};
     // occupancy polls without copies or events: poll q's counter is
     // d_ctr[1 + q % kRing]; the device writes tag(q) << 40 | occupied lanes to
     // h_poll[q % kRing] (pinned, device-mapped at d_poll) and the host waits on it
