@@ -83,6 +83,17 @@ struct Msg<true> {
     using out = double*;
 };
 
+// Whole-line lane policy (full_lanes bit 0): a lane with no codeword, or a
+// finished one, still runs when its 16-lane group -- one 128-byte line of
+// every 512-byte message segment -- holds a lane that is being decoded, so
+// message stores cover whole lines; lines without one are neither read nor
+// written (a partly filled last tile, a draining pool).  Their values are
+// never read.
+__device__ __forceinline__ bool line_occupied(uint64_t m, int lane)
+{
+    return ((m >> (lane & ~15)) & 0xFFFFull) != 0ull;
+}
+
 // The finished codeword's hard bits of the wave's CPW consecutive columns
 // (pre-update ballots), one CPW-byte store per lane when the output is
 // aligned for it (Refill::hard_vec), else byte stores.
@@ -444,7 +455,7 @@ __device__ __forceinline__ void check_bp_block(typename Msg<INPLACE>::in dmsg, t
     const uint64_t act = SYN ? rs.cs.occupied[t] : active[t];
     // full_lanes: converged / empty lanes of an active tile run along on their
     // stale state so every c2v store covers whole lines (their values are never read)
-    const bool run = row < M && ((full_lanes & 1) ? act != 0 : ((act >> lane) & 1ull));
+    const bool run = row < M && ((full_lanes & 1) ? line_occupied(act, lane) : ((act >> lane) & 1ull));
     if constexpr (!SYN) {
         if (!run) return;
     }
@@ -507,7 +518,7 @@ __global__ __launch_bounds__(256, 2) void k_check_bp_first(const double* __restr
     const int32_t row = (int32_t)blockIdx.x * 4 + wave_id();
     const int64_t t = t0 + blockIdx.y;
     const uint64_t act = active[t];
-    const bool run = row < M && ((full_lanes & 1) ? act != 0 : ((act >> lane) & 1ull));
+    const bool run = row < M && ((full_lanes & 1) ? line_occupied(act, lane) : ((act >> lane) & 1ull));
     if (!run) return;
     const double* __restrict__ pt = prior + (size_t)t * N * TILE + lane;
     const int32_t* __restrict__ cols = col_idx + (size_t)row * DC;
@@ -766,7 +777,7 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
         // only hands out finished codewords (no live or refilled lane), nor
         // for refills whose first check reads the prior (Refill::prior_only)
         const bool skip_init = CONT && rf.prior_only && !live;
-        if (!skip_init && (((full_lanes & 1) && touched) || fr || live)) {
+        if (!skip_init && (((full_lanes & 1) && line_occupied(touched, lane)) || fr || live)) {
 #pragma unroll
             for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
         }
@@ -934,7 +945,7 @@ __global__ __launch_bounds__(256) void k_check_msa(typename Msg<INPLACE>::in v2c
     const uint64_t act = SYN ? rs.cs.occupied[t] : active[t];
     // full_lanes: converged / empty lanes of an active tile run along on their
     // stale state so every c2v store covers whole lines (their values are never read)
-    const bool run = row < M && ((full_lanes & 1) ? act != 0 : ((act >> lane) & 1ull));
+    const bool run = row < M && ((full_lanes & 1) ? line_occupied(act, lane) : ((act >> lane) & 1ull));
     if constexpr (!SYN) {
         if (!run) return;
     }
@@ -1178,7 +1189,7 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     const int32_t row = blockIdx.x * 4 + wave_id();
     const int64_t t = t0 + blockIdx.y;
     const uint64_t act = SYN ? rs.cs.occupied[t] : active[t];
-    const bool run = row < M && ((full_lanes & 1) ? act != 0 : ((act >> lane) & 1ull));
+    const bool run = row < M && ((full_lanes & 1) ? line_occupied(act, lane) : ((act >> lane) & 1ull));
     if constexpr (!SYN) {
         if (!run) return;
     }
@@ -1348,7 +1359,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
             if (post) post[pj] = L;
         }
         if (CONT && frm != 0ull && ((full_lanes & 4) || fr)) prior[pj] = np;
-        if (((full_lanes & 1) && touched) || fr || live) {  // as k_var_m
+        if (((full_lanes & 1) && line_occupied(touched, lane)) || fr || live) {  // as k_var_m
 #pragma unroll
             for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
         }
