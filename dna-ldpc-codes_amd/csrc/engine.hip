@@ -1360,6 +1360,9 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                 else
                     LAUNCH(K_CHECK, klaunch((k_check_bp_first<72, false>), grid, dim3(256), 0, stream, prior,
                                             d_col_idx, c2v, active, d_csc_pos, M, N, (int64_t)g->E, t0, full_lanes));
+            } else if (s == 0) {
+                // step 0: the reset left every lane empty and the syndrome
+                // launch above only claims codewords, so no lane is active
             } else if ((rc = launch_check(stream, c2v, t0, gt))) {
                 return rc;
             }
