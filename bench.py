@@ -289,6 +289,11 @@ def main():
         # variable phase reads the codes, the records once, N LLR, writes E
         # v->c fp64 + N/8 hard-bit ballots
         by_kernel = {"check": 9.0 * E + 16.0 * M, "variable": 9.0 * E + 16.0 * M + 8.0 * N + N / 8.0}
+        if getattr(eng, "msa_meta", False):
+            # no per-edge codes: the check phase writes one 16-bit meta word per
+            # row, the variable phase reads it and its columns' sign bytes, and
+            # writes the sign bytes with the v2c (2 N)
+            by_kernel = {"check": 8.0 * E + 18.0 * M, "variable": 8.0 * E + 18.0 * M + 10.0 * N + N / 8.0}
     else:
         by_kernel = {
             # check phase: read E v->c (d) + write E c->v (lr), fp64
@@ -381,7 +386,8 @@ def main():
                    "algo": algo, "parallelism": f"dp{world} (contiguous codeword shards, no collective)",
                    "resident_per_pass": eng.cap, "group_tiles": eng.group_tiles, "nontemporal_d": eng.nontemporal,
                    "two_stream": eng.pipeline, "continuous": eng.continuous, "resident_pool": eng.resident,
-                   "compressed_msa": eng.msa_compressed, "syndrome_split": eng.syndrome_split,
+                   "compressed_msa": eng.msa_compressed,
+                   "msa_meta": getattr(eng, "msa_meta", False), "syndrome_split": eng.syndrome_split,
                    "pingpong": eng.pingpong,
                    "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 4)},
         "roofline": roof,

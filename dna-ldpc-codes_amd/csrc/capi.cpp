@@ -698,7 +698,8 @@ int ldpc_engine_info(ldpc_engine* e, int64_t* cap, int64_t* group_tiles, int32_t
     if (flags) *flags = (e->e->nt_d ? 1 : 0) | (e->e->pipe ? 2 : 0) | (e->e->lr_csc ? 4 : 0) | (e->e->cont ? 8 : 0) |
                         (e->e->msa_c ? 16 : 0) | (e->e->res ? 32 : 0) | (e->e->syn_split ? 64 : 0) |
                         (e->e->syn_fused ? 128 : 0) | (e->e->res && e->e->tile_streams ? 256 : 0) |
-                        (e->e->res && e->e->pingpong ? 512 : 0) | (e->e->xr ? 1024 : 0);
+                        (e->e->res && e->e->pingpong ? 512 : 0) | (e->e->xr ? 1024 : 0) |
+                        (e->e->msa_meta ? 2048 : 0);
     return LDPC_OK;
 }
 

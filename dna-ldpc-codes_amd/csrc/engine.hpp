@@ -48,6 +48,8 @@ struct Engine {
     int pp_cpw = 4;           // pingpong: variable-phase columns per wave (LDPC_PP_CPW)
     int var_cpw = 1;          // variable phase: columns per wave (k_var_m when > 1)
     bool msa_c = false;       // min-sum with compressed c2v (records + codes, k_check_msa_c / k_var_msa_c)
+    bool msa_meta = false;    // msa_c: per-row meta byte + variable-owned sign bytes instead of per-edge codes (LDPC_MSA_META)
+    uint8_t* d_sgn = nullptr; // msa_meta: [tile][N][64] sign bits of the v2c each column last stored
     bool res = false;         // resident pool: a few tiles iterated in place (c2v overwrites v2c), syndrome in the check kernel
     int res_poll = 4;         // res: steps between occupancy polls
     int res_syn_split = 0;    // res: 0 = syndrome fused into the check kernel, >0 = k_syndrome_split blocks per tile

@@ -278,7 +278,8 @@ __global__ __launch_bounds__(256) void k_init(const double* __restrict__ in, int
                                               const int32_t* __restrict__ col_ptr, const int32_t* __restrict__ col_edge,
                                               double* __restrict__ prior, double* __restrict__ v2c,
                                               uint64_t* __restrict__ hard, uint64_t* __restrict__ active,
-                                              int32_t* __restrict__ iters, uint8_t* __restrict__ valid)
+                                              int32_t* __restrict__ iters, uint8_t* __restrict__ valid,
+                                              uint8_t* __restrict__ sgn)
 {
     __shared__ double s[TILE][TILE + 1];
     const int lane = lane_id(), w = wave_id();
@@ -312,6 +313,8 @@ __global__ __launch_bounds__(256) void k_init(const double* __restrict__ in, int
         prior[((size_t)t * N + j) * TILE + lane] = pv;
         const int32_t a = col_ptr[j], e1 = col_ptr[j + 1];
         for (int32_t q = a; q < e1; ++q) v2c[((size_t)t * E + col_edge[q]) * TILE + lane] = m;
+        // compressed min-sum without codes: sign bits of the stored v2c (all edges alike)
+        if (sgn) sgn[((size_t)t * N + j) * TILE + lane] = (m >= 0) ? 0u : 0xffu;
         const uint64_t hm = __ballot(h && inb);
         if (lane == 0) hard[(size_t)t * N + j] = hm;
     }
@@ -1132,7 +1135,8 @@ constexpr int MSA_REC_PLANES = 4;
 
 template <int DC, bool NT>
 __device__ __forceinline__ void check_msa_c_row(const double* __restrict__ v2c, uint8_t* __restrict__ codes,
-                                                double* __restrict__ rec, int32_t M, int64_t E, int64_t t, int32_t row)
+                                                double* __restrict__ rec, uint16_t* __restrict__ meta, int32_t M,
+                                                int64_t E, int64_t t, int32_t row)
 {
     const int lane = lane_id();
     const double* __restrict__ src = v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
@@ -1166,6 +1170,16 @@ __device__ __forceinline__ void check_msa_c_row(const double* __restrict__ v2c, 
     r[TILE] = m2;
     if (nan0) r[2 * TILE] = a0;
     if (nan1) r[3 * TILE] = a1;
+    if (meta) {
+        // MSA-C without codes: 16 bits per (row, lane) -- bit 15 the row's sign
+        // parity, bit 9 NaN at x_1, bit 8 NaN at x_0, bits 0-7 i1 (0xff: no
+        // minimum, every |x| inf or NaN).  The variable phase rebuilds each
+        // edge's code from it, the edge's position k in the row and the sign
+        // bit it stored itself with the v2c (the same !(x >= 0) as negb).
+        meta[((size_t)blockIdx.y * M + row) * TILE + lane] =
+            (uint16_t)((neg << 15) | ((nan1 ? 1u : 0u) << 9) | ((nan0 ? 1u : 0u) << 8) | (i1 < 0 ? 0xffu : (uint32_t)i1));
+        return;
+    }
     uint8_t* __restrict__ c = codes + ((size_t)blockIdx.y * E + (size_t)row * DC) * TILE + lane;
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
@@ -1181,7 +1195,8 @@ __device__ __forceinline__ void check_msa_c_row(const double* __restrict__ v2c, 
 // previous variable phase's ballots, every block ends in res_arrive.
 template <int DC, bool NT, bool SYN>
 __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, uint8_t* __restrict__ codes,
-                                                     double* __restrict__ rec, const uint64_t* __restrict__ active,
+                                                     double* __restrict__ rec, uint16_t* __restrict__ meta,
+                                                     const uint64_t* __restrict__ active,
                                                      int32_t M, int64_t E, int64_t t0, int full_lanes, ResStep rs)
 {
     static_assert(DC >= 2 && DC <= 96, "row degree");
@@ -1203,7 +1218,7 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
         }
         if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
     }
-    if (run) check_msa_c_row<DC, NT>(v2c, codes, rec, M, E, t, row);
+    if (run) check_msa_c_row<DC, NT>(v2c, codes, rec, meta, M, E, t, row);
     if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0, gridDim.x);
 }
 
@@ -1212,14 +1227,19 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
 // Workgroups are dispatched to the 8 XCDs round-robin, so when gt divides 8
 // every XCD only ever touches the records of one tile (2 MB), which stay in
 // its 4 MB L2 while they are re-read by the tile's 72 columns per row.
-template <int DV, bool NT, bool CONT, int CPW, bool SEL2 = false>
+// META (meta != nullptr at the check): codes rebuilt from the row's 16-bit meta word,
+// the edge's position k in its row (edges are numbered row-major, k = e - 72 r)
+// and the sign byte this kernel stored with the column's v2c (sgn, one bit per
+// edge: the check's sign bit is !(x >= 0) of exactly that value); no code
+// bytes are written or read.
+template <int DV, bool NT, bool CONT, int CPW, bool SEL2 = false, bool META = false>
 __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ codes, const double* __restrict__ rec,
                                                    double* __restrict__ v2c, double* __restrict__ prior,
                                                    uint64_t* __restrict__ hard, const uint64_t* __restrict__ active,
                                                    const int32_t* __restrict__ col_edge,
                                                    const int32_t* __restrict__ col_row, double* __restrict__ post,
                                                    int32_t N, int32_t M, int64_t E, int64_t t0, uint32_t gt, Refill rf,
-                                                   int full_lanes)
+                                                   int full_lanes, const uint16_t* __restrict__ meta, uint8_t* sgn)
 {
     const int lane = lane_id();
     const uint32_t ty = blockIdx.x % gt;
@@ -1260,12 +1280,44 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
         for (int c = 0; c < CPW; ++c) xin[c] = in_row[j0 + c];
     }
     if (live) {
-        uint32_t cd[CPW][DV];
+        // codes: one byte per edge (cd), or with META one 4-bit code per edge
+        // packed 8 to a register (cpk; fewer VGPRs live across the gathers)
+        uint32_t cd[META ? 1 : CPW][DV], cpk[CPW];
+        auto code = [&](int c, int s) -> uint32_t {
+            if constexpr (META) return (cpk[c] >> (4 * s)) & 15u;
+            else return cd[c][s];
+        };
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             pv[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
+            if constexpr (!META) {
 #pragma unroll
-            for (int s = 0; s < DV; ++s) cd[c][s] = cg[(size_t)eid[c][s] * TILE];
+                for (int s = 0; s < DV; ++s) cd[META ? 0 : c][s] = cg[(size_t)eid[c][s] * TILE];
+            }
+        }
+        if constexpr (META) {
+            constexpr int32_t DCR = 72;  // row degree (MSA-C runs on the (8,72)-regular graph only)
+            const uint16_t* __restrict__ mg = meta + (size_t)ty * M * TILE + lane;
+            uint32_t md[CPW][DV], sb[CPW];
+#pragma unroll
+            for (int c = 0; c < CPW; ++c) {
+                sb[c] = sgn[((size_t)t * N + j0 + c) * TILE + lane];
+#pragma unroll
+                for (int s = 0; s < DV; ++s) md[c][s] = mg[(size_t)rid[c][s] * TILE];
+            }
+            // code of edge k (as check_msa_c_row's): sign = parity ^ own sign,
+            // plane = NaN at the first other edge ? 3 (k = 0) / 2 : k == i1
+#pragma unroll
+            for (int c = 0; c < CPW; ++c)
+#pragma unroll
+                for (int s = 0; s < DV; ++s) {
+                    const uint32_t m = md[c][s];
+                    const uint32_t k = (uint32_t)(eid[c][s] - rid[c][s] * DCR);
+                    const uint32_t nanf = (m >> (k == 0 ? 9 : 8)) & 1u;
+                    const uint32_t pl = nanf ? (k == 0 ? 3u : 2u) : ((m & 0xffu) == k ? 1u : 0u);
+                    const uint32_t q = ((m >> 15) ^ ((sb[c] >> s) & 1u)) | (pl << 1);
+                    cpk[c] = (s == 0 ? 0u : cpk[c]) | (q << (4 * s));
+                }
         }
         if constexpr (SEL2) {
             // min1 and min2 planes both loaded (whole 512-B segments, no
@@ -1284,7 +1336,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
             for (int c = 0; c < CPW; ++c)
 #pragma unroll
                 for (int s = 0; s < DV; ++s) {
-                    const uint32_t sp = (cd[c][s] >> 1) & 3u;
+                    const uint32_t sp = (code(c, s) >> 1) & 3u;
                     l[c][s] = (sp & 1u) ? mb[c][s] : ma[c][s];
                     nanm |= sp >> 1;
                 }
@@ -1293,7 +1345,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
                 for (int c = 0; c < CPW; ++c)
 #pragma unroll
                     for (int s = 0; s < DV; ++s) {
-                        const uint32_t sp = (cd[c][s] >> 1) & 3u;
+                        const uint32_t sp = (code(c, s) >> 1) & 3u;
                         const size_t o = ((size_t)rid[c][s] * MSA_REC_PLANES + (sp | 2u)) * TILE;
                         const double nv = rg[o];  // harmless extra read for lanes that do not use it
                         if (sp >= 2) l[c][s] = nv;
@@ -1305,7 +1357,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
             for (int c = 0; c < CPW; ++c)
 #pragma unroll
                 for (int s = 0; s < DV; ++s) {
-                    const uint32_t sp = (cd[c][s] >> 1) & 3u;
+                    const uint32_t sp = (code(c, s) >> 1) & 3u;
                     l[c][s] = rg[((size_t)rid[c][s] * MSA_REC_PLANES + sp) * TILE];
                 }
         }
@@ -1313,7 +1365,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
         for (int c = 0; c < CPW; ++c)
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
-                const int sign = (cd[c][s] & 1u) ? -1 : 1;
+                const int sign = (code(c, s) & 1u) ? -1 : 1;
                 l[c][s] = (double)sign * l[c][s];
             }
     }
@@ -1362,6 +1414,12 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
         if (((full_lanes & 1) && line_occupied(touched, lane)) || fr || live) {  // as k_var_m
 #pragma unroll
             for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
+            if constexpr (META) {
+                uint32_t sbn = 0;
+#pragma unroll
+                for (int s = 0; s < DV; ++s) sbn |= (dv[s] >= 0 ? 0u : 1u) << s;
+                sgn[pj] = (uint8_t)sbn;
+            }
         }
         const uint64_t m = __ballot(h);
         if (lane == 0 && touched) {

@@ -463,6 +463,7 @@ class Engine:
         self.tile_streams = bool(fl.value & 256)  # resident pool, one stream per tile (LDPC_RES_STREAMS)
         self.pingpong = bool(fl.value & 512)  # resident BP pool, check(t) + variable(t-1) per launch (LDPC_PINGPONG)
         self.xcd_resident = bool(fl.value & 1024)  # one persistent launch, slots in the XCDs' L2 (LDPC_XR)
+        self.msa_meta = bool(fl.value & 2048)  # MSA-C without per-edge codes: 16-bit meta word per row (LDPC_MSA_META)
 
     def decode(self, d_in, in_kind: int, B: int, max_iter: int, d_hard=None, d_post=None, post_kind=POST_LLR,
                d_iters=None, d_valid=None):

@@ -232,7 +232,9 @@ int ldpc_engine_set_params(ldpc_engine *e, int32_t msa_precision, double msa_ste
  * (env LDPC_SYN_FUSED); bit 8 = resident pool with one HIP stream per pool
  * tile (env LDPC_RES_STREAMS; the tiles' kernels run concurrently); bit 9 =
  * resident BP pool, ping-pong launches (env LDPC_PINGPONG); bit 10 = the
- * XCD-resident BP decoder for array codes (env LDPC_XR). */
+ * XCD-resident BP decoder for array codes (env LDPC_XR);
+ * bit 11 = compressed min-sum without per-edge codes: one 16-bit meta word per row,
+ * sign bits kept by the variable phase (env LDPC_MSA_META). */
 int ldpc_engine_info(ldpc_engine *e, int64_t *cap, int64_t *group_tiles, int32_t *flags);
 int ldpc_engine_stats(ldpc_engine *e, ldpc_kernel_stats *out);
 /* Device time of whole decodes with concurrent tile streams (bit 8 of

@@ -354,16 +354,21 @@ def test_continuous_batching_edge_cases(gpu, og, codewords, monkeypatch, chunk):
     _cmp(G2, og, llr[:130], 12, algo="msa", chunk=chunk)
 
 
-@pytest.mark.parametrize("msa_c,group,cont,cpw", [(0, 3, 1, 4), (1, 1, 0, 1), (1, 2, 1, 2), (1, 3, 0, 4), (1, 8, 1, 4),
-                                                  (1, 0, 0, 2), (1, 2, 1, 8)])
-def test_min_sum_compressed_messages_bitexact(gpu, og, codewords, monkeypatch, msa_c, group, cont, cpw):
+@pytest.mark.parametrize("msa_c,group,cont,cpw,meta", [(0, 3, 1, 4, 1), (1, 1, 0, 1, 1), (1, 2, 1, 2, 1), (1, 3, 0, 4, 1),
+                                                       (1, 8, 1, 4, 1), (1, 0, 0, 2, 1), (1, 2, 1, 8, 1), (1, 3, 0, 4, 0),
+                                                       (1, 8, 1, 4, 0)])
+def test_min_sum_compressed_messages_bitexact(gpu, og, codewords, monkeypatch, msa_c, group, cont, cpw, meta):
     """MSA-C (kernels.hpp k_check_msa_c / k_var_msa_c): the check phase stores
-    per row the four magnitudes min1 / min2 / |x_0| / |x_1| and per edge a sign +
-    source code; the variable phase rebuilds each c2v by the reference's
-    expression, so hard bits, iterations, valid flags and the posterior L stay
-    bit-exact -- across group sizes (XCD-affine tile order), continuous
-    batching, columns per wave, and the NaN / inf first-other-edge cases."""
+    per row the four magnitudes min1 / min2 / |x_0| / |x_1| and either per edge
+    a sign + source code (meta 0) or per row one 16-bit meta word (sign parity,
+    NaN at x_0 / x_1, index of min1) while the variable phase keeps the sign
+    bits of the v2c it stored (meta 1, an option); the
+    variable phase rebuilds each c2v by the reference's expression, so hard
+    bits, iterations, valid flags and the posterior L stay bit-exact -- across
+    group sizes (XCD-affine tile order), continuous batching, columns per wave,
+    and the NaN / inf / -0.0 first-other-edge cases."""
     monkeypatch.setenv("LDPC_MSA_C", str(msa_c))
+    monkeypatch.setenv("LDPC_MSA_META", str(meta))
     monkeypatch.setenv("LDPC_GROUP_TILES", str(group))
     monkeypatch.setenv("LDPC_CONT", str(cont))
     monkeypatch.setenv("LDPC_VAR_CPW", str(cpw))
