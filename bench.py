@@ -290,10 +290,10 @@ def main():
         # v->c fp64 + N/8 hard-bit ballots
         by_kernel = {"check": 9.0 * E + 16.0 * M, "variable": 9.0 * E + 16.0 * M + 8.0 * N + N / 8.0}
         if getattr(eng, "msa_meta", False):
-            # no per-edge codes: the check phase writes one 16-bit meta word per
+            # no per-edge codes: the check phase writes one 32-bit meta word per
             # row, the variable phase reads it and its columns' sign bytes, and
             # writes the sign bytes with the v2c (2 N)
-            by_kernel = {"check": 8.0 * E + 18.0 * M, "variable": 8.0 * E + 18.0 * M + 10.0 * N + N / 8.0}
+            by_kernel = {"check": 8.0 * E + 20.0 * M, "variable": 8.0 * E + 20.0 * M + 10.0 * N + N / 8.0}
     else:
         by_kernel = {
             # check phase: read E v->c (d) + write E c->v (lr), fp64

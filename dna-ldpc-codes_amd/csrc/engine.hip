@@ -53,7 +53,7 @@ constexpr int64_t kDefaultResStreams = 0;    // LDPC_RES_STREAMS: resident pool,
 constexpr int64_t kDefaultResSyn = 0;        // LDPC_RES_SYN: resident pool syndrome, 0 = fused into the check kernel, >0 = k_syndrome_split blocks per tile
 constexpr int64_t kDefaultSynSplit = 32;     // LDPC_SYN_SPLIT: syndrome blocks per tile in continuous mode (0: one block, k_syndrome_cont; A/B min-sum config 5 +5-6 %)
 constexpr int64_t kDefaultSynFused = 0;      // LDPC_SYN_FUSED: grouped continuous mode, syndrome fused into the check kernel
-constexpr int64_t kDefaultMsaMeta = 0;  // LDPC_MSA_META: MSA-C without per-edge code bytes (16-bit meta word per row, sign bytes per column; A/B config 5 -1.5 %)
+constexpr int64_t kDefaultMsaMeta = 1;  // LDPC_MSA_META: MSA-C without per-edge code bytes (32-bit meta word per row, sign bytes per column; config 5 A/B +2-3 %)
 constexpr int64_t kDefaultResMsaC = 0;       // LDPC_RES_MSA_C: resident pool for compressed min-sum
 constexpr int64_t kDefaultResTilesMsaC = 2;  // LDPC_RES_TILES_MSA_C: its pool tiles   // LDPC_RES_POLL: steps between occupancy polls
 constexpr int64_t kDefaultPingpong = 0;      // LDPC_PINGPONG: resident BP pool, check(t) + variable(t-1) per launch
@@ -301,7 +301,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     if (res) {
         c2v_tiles = cap_tiles;
         if (msa_c)  // codes + records of the whole pool (13.6 MB per tile for the DNA code)
-            LDPC_HIP(hipMalloc((void**)&c2v, (size_t)cap_tiles * 64 * (E + (size_t)g->M * (dev::MSA_REC_PLANES * 8 + 2))));
+            LDPC_HIP(hipMalloc((void**)&c2v, (size_t)cap_tiles * 64 * (E + (size_t)g->M * (dev::MSA_REC_PLANES * 8 + 4))));
         else
             c2v = v2c;  // in place
     } else {
@@ -309,7 +309,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         LDPC_HIP(hipMalloc((void**)&c2v, (size_t)c2v_tiles * 64 * E * sizeof(double)));
     }
     LDPC_HIP(hipMalloc((void**)&prior, (size_t)cap * g->N * sizeof(double)));
-    msa_meta = msa_c && env_int("LDPC_MSA_META", kDefaultMsaMeta) != 0;
+    msa_meta = msa_c && E < (size_t)dev::MSA_META_NONE && env_int("LDPC_MSA_META", kDefaultMsaMeta) != 0;
     if (msa_meta) LDPC_HIP(hipMalloc((void**)&d_sgn, (size_t)cap * g->N));
     LDPC_HIP(hipMalloc((void**)&hard, (size_t)cap_tiles * g->N * sizeof(uint64_t)));
     LDPC_HIP(hipMalloc((void**)&active, (size_t)cap_tiles * sizeof(uint64_t)));
@@ -619,17 +619,17 @@ static double* msa_rec(double* scratch, int64_t tiles, int64_t E)
     return reinterpret_cast<double*>(reinterpret_cast<uint8_t*>(scratch) + (size_t)tiles * E * 64);
 }
 
-// then (msa_meta) the meta words [c2v_tiles][M][64] u16
-static uint16_t* msa_meta_p(double* scratch, int64_t tiles, int64_t E, int32_t M)
+// then (msa_meta) the meta words [c2v_tiles][M][64] u32
+static uint32_t* msa_meta_p(double* scratch, int64_t tiles, int64_t E, int32_t M)
 {
-    return reinterpret_cast<uint16_t*>(msa_rec(scratch, tiles, E) + (size_t)tiles * M * dev::MSA_REC_PLANES * 64);
+    return reinterpret_cast<uint32_t*>(msa_rec(scratch, tiles, E) + (size_t)tiles * M * dev::MSA_REC_PLANES * 64);
 }
 
 template <bool NT, int CPW>
 static void var_msa_c(hipStream_t s, unsigned nb, const uint8_t* codes, const double* rec, double* v2c, double* prior,
                       uint64_t* hard, const uint64_t* active, const int32_t* col_edge, const int32_t* col_row,
                       double* pt, int32_t N, int32_t M, int64_t E, int64_t t0, unsigned gt, const dev::Refill& rf,
-                      int full, const uint16_t* meta, uint8_t* sgn)
+                      int full, const uint32_t* meta, uint8_t* sgn)
 {
     using namespace dev;
     if (rf.fresh && meta)
@@ -655,7 +655,7 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
     const dim3 grid((M + 3) / 4, gt), blk(256);
     // the resident pool writes the check messages over the variable messages
     const bool inplace = scratch == v2c;
-    uint16_t* mmeta = msa_meta ? msa_meta_p(scratch, c2v_tiles, E, M) : nullptr;
+    uint32_t* mmeta = msa_meta ? msa_meta_p(scratch, c2v_tiles, E, M) : nullptr;
     if (inplace && (msa_c || !reg72)) { set_error("in-place check phase needs the regular fp64 kernels"); return LDPC_ERR_ARG; }
     if ((res || syn_fused) && rstep) {  // syndrome + lane bookkeeping fused (ResStep)
         if (msa_c && nt_d)
@@ -745,7 +745,7 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         const unsigned nb = gt * (unsigned)(N / (4 * cpw));
         const uint8_t* codes = msa_codes(scratch);
         const double* rec = msa_rec(scratch, c2v_tiles, E);
-        const uint16_t* mmeta = msa_meta ? msa_meta_p(scratch, c2v_tiles, E, g->M) : nullptr;
+        const uint32_t* mmeta = msa_meta ? msa_meta_p(scratch, c2v_tiles, E, g->M) : nullptr;
         LAUNCH_ON(s, K_VAR, {
             if (nt_d) {
                 if (cpw == 1) var_msa_c<true, 1>(s, nb, codes, rec, v2c, prior, hard, active, d_col_edge, d_col_row, pt, N, g->M, E, t0, gt, rf, full_lanes, mmeta, d_sgn);

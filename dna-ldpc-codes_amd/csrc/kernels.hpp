@@ -1132,10 +1132,11 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
 // resident in the XCD's L2; see k_var_msa_c for the XCD-affine tile order).
 // ---------------------------------------------------------------------------
 constexpr int MSA_REC_PLANES = 4;
+constexpr uint32_t MSA_META_NONE = 0x3ffffu;  // meta: no min1 (edge ids must stay below it)
 
 template <int DC, bool NT>
 __device__ __forceinline__ void check_msa_c_row(const double* __restrict__ v2c, uint8_t* __restrict__ codes,
-                                                double* __restrict__ rec, uint16_t* __restrict__ meta, int32_t M,
+                                                double* __restrict__ rec, uint32_t* __restrict__ meta, int32_t M,
                                                 int64_t E, int64_t t, int32_t row)
 {
     const int lane = lane_id();
@@ -1171,13 +1172,15 @@ __device__ __forceinline__ void check_msa_c_row(const double* __restrict__ v2c, 
     if (nan0) r[2 * TILE] = a0;
     if (nan1) r[3 * TILE] = a1;
     if (meta) {
-        // MSA-C without codes: 16 bits per (row, lane) -- bit 15 the row's sign
-        // parity, bit 9 NaN at x_1, bit 8 NaN at x_0, bits 0-7 i1 (0xff: no
-        // minimum, every |x| inf or NaN).  The variable phase rebuilds each
-        // edge's code from it, the edge's position k in the row and the sign
-        // bit it stored itself with the v2c (the same !(x >= 0) as negb).
+        // MSA-C without codes: 32 bits per (row, lane) -- bit 31 the row's sign
+        // parity, bit 30 NaN at x_1, bit 29 NaN at x_0, bits 0-17 the edge id
+        // of min1 (row * DC + i1; MSA_META_NONE: no minimum, every |x| inf or
+        // NaN).  The variable phase rebuilds each edge's code from it, its
+        // own edge id and the sign bit it stored itself with the v2c (the same
+        // !(x >= 0) as negb).
         meta[((size_t)blockIdx.y * M + row) * TILE + lane] =
-            (uint16_t)((neg << 15) | ((nan1 ? 1u : 0u) << 9) | ((nan0 ? 1u : 0u) << 8) | (i1 < 0 ? 0xffu : (uint32_t)i1));
+            (neg << 31) | ((nan1 ? 1u : 0u) << 30) | ((nan0 ? 1u : 0u) << 29) |
+            (i1 < 0 ? MSA_META_NONE : (uint32_t)(row * DC + i1));
         return;
     }
     uint8_t* __restrict__ c = codes + ((size_t)blockIdx.y * E + (size_t)row * DC) * TILE + lane;
@@ -1195,7 +1198,7 @@ __device__ __forceinline__ void check_msa_c_row(const double* __restrict__ v2c, 
 // previous variable phase's ballots, every block ends in res_arrive.
 template <int DC, bool NT, bool SYN>
 __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, uint8_t* __restrict__ codes,
-                                                     double* __restrict__ rec, uint16_t* __restrict__ meta,
+                                                     double* __restrict__ rec, uint32_t* __restrict__ meta,
                                                      const uint64_t* __restrict__ active,
                                                      int32_t M, int64_t E, int64_t t0, int full_lanes, ResStep rs)
 {
@@ -1227,8 +1230,8 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
 // Workgroups are dispatched to the 8 XCDs round-robin, so when gt divides 8
 // every XCD only ever touches the records of one tile (2 MB), which stay in
 // its 4 MB L2 while they are re-read by the tile's 72 columns per row.
-// META (meta != nullptr at the check): codes rebuilt from the row's 16-bit meta word,
-// the edge's position k in its row (edges are numbered row-major, k = e - 72 r)
+// META (meta != nullptr at the check): codes rebuilt from the row's 32-bit meta word
+// (parity, NaN flags, edge id of min1), the edge's own id
 // and the sign byte this kernel stored with the column's v2c (sgn, one bit per
 // edge: the check's sign bit is !(x >= 0) of exactly that value); no code
 // bytes are written or read.
@@ -1239,7 +1242,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
                                                    const int32_t* __restrict__ col_edge,
                                                    const int32_t* __restrict__ col_row, double* __restrict__ post,
                                                    int32_t N, int32_t M, int64_t E, int64_t t0, uint32_t gt, Refill rf,
-                                                   int full_lanes, const uint16_t* __restrict__ meta, uint8_t* sgn)
+                                                   int full_lanes, const uint32_t* __restrict__ meta, uint8_t* sgn)
 {
     const int lane = lane_id();
     const uint32_t ty = blockIdx.x % gt;
@@ -1296,28 +1299,35 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
             }
         }
         if constexpr (META) {
-            constexpr int32_t DCR = 72;  // row degree (MSA-C runs on the (8,72)-regular graph only)
-            const uint16_t* __restrict__ mg = meta + (size_t)ty * M * TILE + lane;
-            uint32_t md[CPW][DV], sb[CPW];
+            const uint32_t* __restrict__ mg = meta + (size_t)ty * M * TILE + lane;
+            uint32_t sb[CPW], anynan = 0;
 #pragma unroll
             for (int c = 0; c < CPW; ++c) {
                 sb[c] = sgn[((size_t)t * N + j0 + c) * TILE + lane];
 #pragma unroll
-                for (int s = 0; s < DV; ++s) md[c][s] = mg[(size_t)rid[c][s] * TILE];
-            }
-            // code of edge k (as check_msa_c_row's): sign = parity ^ own sign,
-            // plane = NaN at the first other edge ? 3 (k = 0) / 2 : k == i1
-#pragma unroll
-            for (int c = 0; c < CPW; ++c)
-#pragma unroll
                 for (int s = 0; s < DV; ++s) {
-                    const uint32_t m = md[c][s];
-                    const uint32_t k = (uint32_t)(eid[c][s] - rid[c][s] * DCR);
-                    const uint32_t nanf = (m >> (k == 0 ? 9 : 8)) & 1u;
-                    const uint32_t pl = nanf ? (k == 0 ? 3u : 2u) : ((m & 0xffu) == k ? 1u : 0u);
-                    const uint32_t q = ((m >> 15) ^ ((sb[c] >> s) & 1u)) | (pl << 1);
+                    // code of the edge (as check_msa_c_row's): sign = parity ^
+                    // own sign, plane 1 iff it is the row's min1 edge
+                    const uint32_t m = mg[(size_t)rid[c][s] * TILE];
+                    anynan |= m;
+                    const uint32_t q = ((m >> 31) ^ ((sb[c] >> s) & 1u)) |
+                                       ((m & MSA_META_NONE) == (uint32_t)eid[c][s] ? 2u : 0u);
                     cpk[c] = (s == 0 ? 0u : cpk[c]) | (q << (4 * s));
                 }
+            }
+            if (__builtin_expect(__ballot((anynan >> 29) & 3u) != 0ull, 0)) {
+                // a row with NaN at x_0 / x_1: planes 3 (k = 0) / 2 (k > 0)
+                constexpr int32_t DCR = 72;  // row degree (MSA-C runs on the (8,72)-regular graph only)
+#pragma unroll
+                for (int c = 0; c < CPW; ++c)
+#pragma unroll
+                    for (int s = 0; s < DV; ++s) {
+                        const uint32_t m = mg[(size_t)rid[c][s] * TILE];
+                        const bool first = eid[c][s] % DCR == 0;  // edges are numbered row-major
+                        if ((m >> (first ? 30 : 29)) & 1u)
+                            cpk[c] = (cpk[c] & ~(6u << (4 * s))) | ((first ? 3u : 2u) << (4 * s + 1));
+                    }
+            }
         }
         if constexpr (SEL2) {
             // min1 and min2 planes both loaded (whole 512-B segments, no
