@@ -9,21 +9,28 @@ Workload (SURVEY 8(d) config 3, weak-scaled per GPU by default): every
 rank decodes its own contiguous shard of `--batch-per-gpu` codewords
 [rank*B, (rank+1)*B) -- or, with `--global-batch G` (config 4: `--gpus 8
 --global-batch 1000000`), its dist.shard of [0, G), "scaling": "strong" --
-from the counter-based BSC(p=0.02) generator (transmitted
-word codeword_n18432_m1860_{1 + b mod 272}, LLR = +-ln49, LR = exp(LLR) by the
+from the counter-based BSC(p=0.02) generator (transmitted word
+codeword_n18432_m1860_{1 + b mod 272}, LLR = +-ln49, LR = exp(LLR) by the
 host libm as DNA_main.cpp:1344 does).  p = 0.02 never converges, so every
 codeword runs exactly 50 iterations.  Inputs are generated into HBM before the
 timed region; a step = one full decode of the shard (init, 50 x [syndrome,
 check, variable], final syndrome, hard-bit unpack, iteration counts).
 
-No data-path collective: ranks only meet in a barrier and a MAX of their
-elapsed times (gloo, CPU tensors).  `value` = all codewords of all ranks /
-max elapsed.
+No data-path collective: ranks only meet in a barrier, a MAX of their elapsed
+times and a gather of their check counts (gloo, CPU tensors).  `value` = all
+codewords of all ranks / max elapsed.
 
-Correctness of the timed decode: at N = 1 the cpu_baseline leg decodes a
-sample of the same workload with the oracle and compares hard bits,
-iteration counts and valid flags of every sampled codeword with the GPU's
-(`check` in the JSON line); any mismatch exits non-zero.
+Correctness of the timed decode, on every rank: the oracle decodes a sample of
+the rank's own shard (at N = 1 the cpu_baseline leg's sample, at N > 1 about
+16 codewords per host thread of the rank's share of the cores, from both ends
+of the shard) and its hard bits, iteration counts and valid flags must equal
+the GPU's; `check` in the JSON line carries the per-rank counts and any
+mismatch exits non-zero.
+
+At N = 1 (unless --secondary 0) two driver-timed secondary legs follow the
+headline, each with its own oracle check, under "secondary": config 2 (the
+272-codeword DNA batch through the host API ldpc_decode, median of 15 calls)
+and config 5 (1M codewords, min-sum with early exit, 2 timed steps).
 """
 from __future__ import annotations
 
@@ -42,6 +49,7 @@ sys.path[:0] = [os.path.join(ROOT, "dna-ldpc-codes_amd")]
 
 METRIC = "decoded codewords/sec (n=18432, m=2048, 50 BP iters) at 1/2/4/8 GPUs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+VAR_CPW = 4  # the engine's default columns per variable-phase wave (kernel instantiation names)
 
 
 def parse():
@@ -64,27 +72,198 @@ def parse():
     ap.add_argument("--chunk", type=int, default=0, help="resident codewords per pass (0: auto)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--check-per-thread", type=int, default=16,
+                    help="N > 1 (and --cpu-baseline 0): oracle-checked codewords per host thread of each rank")
     ap.add_argument("--group-tiles", type=int, default=-1, help="tiles per check/variable launch (-1: engine default)")
     ap.add_argument("--nt", type=int, default=-1, help="nontemporal d-stream (-1: engine default)")
-    ap.add_argument("--pipe", type=int, default=-1, help="two-stream check/variable overlap (-1: engine default)")
     ap.add_argument("--cont", type=int, default=-1, help="continuous batching / lane refill (-1: engine default)")
     ap.add_argument("--res", type=int, default=-1,
                     help="resident in-place pool of a few tiles (-1: engine default; BP / fp64 min-sum, continuous)")
+    ap.add_argument("--var-cpw", type=int, default=0, help="columns per variable-phase wave (0: engine default 4)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
+    ap.add_argument("--secondary", type=int, default=1,
+                    help="N = 1: also time config 2 (DNA batch, host API) and config 5 (1M min-sum) after the headline")
+    ap.add_argument("--msa-batch", type=int, default=1_000_000, help="config-5 secondary leg: codewords")
     ap.add_argument("--workload", default="bsc", choices=["bsc", "dna272"],
                     help="bsc: SURVEY 8(d) configs 3-5 (default); dna272: config 2, the 272-codeword DNA batch")
     return ap.parse_args()
 
 
-def bench_dna272(args):
+def host_cpus() -> dict:
+    """Host threads this process can run at once: the affinity mask, capped by
+    a cgroup CPU quota when there is one (a one-GPU box: 16 of 256)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(math.ceil(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return {"effective": min(aff, quota) if quota else aff, "affinity": aff, "cgroup_quota_cpus": quota}
+
+
+def _oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker / CPU baseline only
+    return oracle
+
+
+def oracle_check(og, llr_fn, gpu_out, algo, max_iter, ranges, threads):
+    """Oracle vs GPU on shard rows `ranges` [(start, n)]: (checked, mismatching
+    rows, oracle seconds, oracle codewords)."""
+    checked, bad, el = 0, [], 0.0
+    for start, n in ranges:
+        if n <= 0:
+            continue
+        llr = llr_fn(start, n)
+        t = time.perf_counter()
+        rh, _, rit, rv = og.decode_batch(llr, max_iter, algo=algo, threads=threads, want_post=False)
+        el += time.perf_counter() - t
+        h, it, v = gpu_out(start, n)
+        for k in range(n):
+            if not (np.array_equal(h[k], rh[k]) and it[k] == rit[k] and bool(v[k]) == bool(rv[k])):
+                bad.append(start + k)
+        checked += n
+    return checked, bad, el
+
+
+def cpu_baseline(args, og, llr_fn, B, gpu_out, cpus):
+    """The oracle (bit-exact C restatement of dec.cpp, 'port') on the host's
+    cores, on a bounded sample of the same workload -- and the check of the
+    timed GPU decode on every sampled codeword.  Returns (cpu_baseline, check)."""
+    threads = cpus["effective"]
+    algo = 0 if args.algo == "bp" else 1
+    # calibrate with one codeword per thread, then size the sample for ~cpu_seconds
+    n0 = min(threads, B)
+    c0, bad0, t1 = oracle_check(og, llr_fn, gpu_out, algo, args.max_iter, [(0, n0)], threads)
+    rounds = max(1, int(args.cpu_seconds / max(t1, 1e-3)))
+    n = max(1, min(threads * rounds, B - n0))
+    start = n0 if B > n0 else 0
+    c1, bad1, el = oracle_check(og, llr_fn, gpu_out, algo, args.max_iter, [(start, n)], threads)
+    cb = {"value": round(n / el, 3), "unit": "codewords/s", "cores": threads, "kind": "port",
+          "per_core": round(n / el / threads, 3),
+          "host": cpus,
+          "sample": f"{n} codewords of the same BSC(p={args.p}) workload (indices {start}..{start + n - 1}), "
+                    f"{args.max_iter} iters, oracle/ldpc_oracle.c on {threads} host threads (the affinity mask "
+                    f"{cpus['affinity']} capped by the cgroup CPU quota {cpus['cgroup_quota_cpus']}), {el:.1f} s"}
+    return cb, (c0 + c1, bad0 + bad1)
+
+
+def kernel_names(eng, algo) -> dict:
+    """Template instantiations of the check / variable kernels an engine
+    launches (csrc/engine.hip launch_check / launch_var), as rocprofv3 names
+    them (tools/pmc_r3.py short form)."""
+    msa = "true" if algo == "msa" else "false"
+    if eng.msa_compressed:
+        return {"check": "k_check_msa_c<72>", "variable": f"k_var_msa_c<72,8,{str(eng.continuous).lower()},4>"}
+    chk = "k_check_msa" if algo == "msa" else "k_check_bp"
+    if eng.resident:
+        return {"check": f"{chk}<72,false,true>", "variable": f"k_var_m<{msa},8,false,true,{VAR_CPW},true>"}
+    nt = str(eng.nontemporal).lower()
+    return {"check": f"{chk}<72,{nt},false>",
+            "variable": f"k_var_m<{msa},8,{nt},{str(eng.continuous).lower()},{VAR_CPW},false>"}
+
+
+def algorithmic_bytes(eng, N, M, E) -> dict:
+    """Algorithmic bytes per executed codeword-iteration, per kernel (SURVEY
+    8(d))."""
+    if eng.msa_compressed:
+        # compressed min-sum: the check phase reads E v->c fp64 and writes per
+        # row a {min1, min2} record + a 32-bit meta word (NaN planes only when
+        # NaN occurs); the variable phase reads the records and meta words,
+        # N LLR and its columns' sign bytes, and writes E v->c fp64, the sign
+        # bytes (N) and N/8 hard-bit ballots
+        return {"check": 8.0 * E + 20.0 * M, "variable": 8.0 * E + 20.0 * M + 10.0 * N + N / 8.0}
+    return {
+        # check phase: read E v->c (d) + write E c->v (lr), fp64
+        "check": 16.0 * E,
+        # variable phase: read E lr + N LR, write E d + N/8 hard-bit ballots
+        "variable": 16.0 * E + 8.0 * N + N / 8.0,
+    }
+
+
+def bound_detail(eng) -> str:
+    if eng.msa_compressed:
+        return ("compressed min-sum (DESIGN.md sec. 4, 9): the check kernel streams its 4-tile group's v2c (302 MB, "
+                "more than the 256 MB Infinity Cache) from HBM; the variable kernel gathers the records and meta "
+                "words from its XCD's L2 and stores the fp64 v2c -- L2-request / issue bound rather than HBM-bound "
+                "(profiles/r3 PMC: L2 requests and VALU per wave); no MFMA")
+    if eng.resident:
+        return ("resident in-place pool sized to the 256 MB Infinity Cache: every message byte crosses the L2 -> "
+                "fabric interface once per phase (PMC fabric bytes = 1.02-1.04 x algorithmic), served by HBM and the "
+                "Infinity Cache; the DRAM-request counters count cache hits too on gfx950 (calibrated), so the cache "
+                "share is not observable; no MFMA")
+    return ("grouped schedule: the group's c2v scratch is meant to stay in the Infinity Cache between the phases, the "
+            "v2c stream goes to HBM (nontemporal); memory-bound, no MFMA")
+
+
+def find_traffic(kname):
+    """L2 -> fabric bytes per codeword-iteration of this exact kernel
+    instantiation from the newest committed PMC summary (profiles/r*/pmc_traffic.json)."""
+    for tf in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
+        tj = json.load(open(tf))
+        per = tj.get("per_cw_iter_by_instantiation", {})
+        if kname in per:
+            return float(per[kname]), os.path.relpath(tf, ROOT)
+    return None, None
+
+
+def roofline(eng, G, st, cw_iters) -> dict:
+    """Roofline of the dominant kernel: algorithmic bytes per launch / its
+    average launch duration (HIP events on the kernel's dispatch packet)."""
+    N, M, E = G.N, G.M, G.E
+    by_kernel = algorithmic_bytes(eng, N, M, E)
+    names = kernel_names(eng, "msa" if eng.algo == 1 else "bp")
+
+    def avg_ms(k):
+        return st[k]["ms"] / st[k]["sampled"] if st[k]["sampled"] else 0.0
+
+    dom = max(("check", "variable"), key=lambda k: avg_ms(k) * st[k]["launches"])
+    k_launch = max(1, st[dom]["launches"])
+    k_avg = avg_ms(dom)
+    bytes_per_launch = by_kernel[dom] * cw_iters / k_launch
+    achieved = bytes_per_launch / (k_avg * 1e-3) / 1e9 if k_avg > 0 else None
+    it_ms = sum(avg_ms(k) * st[k]["launches"] for k in ("check", "variable", "syndrome"))
+    iter_bytes = (32.0 * E + 10.0 * N) * cw_iters
+    per_cwi, traffic_src = find_traffic(names[dom])
+    traffic = round(per_cwi * cw_iters / k_launch) if per_cwi else None
+    # measured ceiling of the access shape (tools/cachebench, profiles/r2/cachebench.txt): one launch per
+    # in-place pass of the check kernel's shape over a 192-224 MB working set (the resident pool's size)
+    ceiling = 6780.0 if eng.resident else None
+    return {
+        "bound": "hbm", "kernel": names[dom], "bound_detail": bound_detail(eng),
+        "ceiling_measured": ceiling,
+        "ceiling_source": ("tools/cachebench: in-place 72 x 512 B per wave, one launch per pass, 192-224 MB "
+                           "working set (profiles/r2/cachebench.txt)") if ceiling else None,
+        "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+        "frac_of_measured_ceiling": round(achieved / ceiling, 4) if (achieved and ceiling) else None,
+        "traffic": traffic,
+        "traffic_source": traffic_src,
+        "traffic_per_cw_iter": per_cwi,
+        "algorithmic_bytes_per_cw_iter": by_kernel[dom],
+        "bytes_per_launch": round(bytes_per_launch), "avg_launch_ms": round(k_avg, 4),
+        "launch_unit": "kernel launch",
+        "iteration_GBps": round(iter_bytes / (it_ms * 1e-3) / 1e9, 1) if it_ms > 0 else None,
+        "kernels": names,
+        "avg_ms": {k: round(avg_ms(k), 4) for k in st},
+        "launches": {k: v["launches"] for k, v in st.items()},
+        "sampled": {k: v["sampled"] for k, v in st.items()},
+    }
+
+
+def dna272(args, og, threads, max_iter=200):
     """Config 2: the 272-codeword DNA-like batch (synth.dna_like_llrs, 72000
-    reads) at the pipeline's max_iter (default 200 here), device-resident
-    (LR = host libm exp, DNA_main.cpp:1344), plus the end-to-end host-API time
-    of the same decode (host exp + PCIe + decode + copy back) -- the in-process
-    replacement of decoder.py's 272 ldpc.exe runs."""
+    reads) at the pipeline's max_iter, device-resident (LR = host libm exp,
+    DNA_main.cpp:1344), plus the end-to-end host-API time of the same decode
+    (LR table / host exp + PCIe + decode + copy back) -- the in-process
+    replacement of decoder.py's 272 ldpc.exe runs (decoder.py:553-562)."""
     import ldpc_amd as L
     import synth
-    max_iter = args.max_iter if args.max_iter != 50 else 200
     cw = synth.load_codewords()
     llr = synth.dna_like_llrs(cw, seed=0)
     uniq, inv = np.unique(llr, return_inverse=True)
@@ -115,98 +294,103 @@ def bench_dna272(args):
     th = []
     for _ in range(15):  # the host leg varies with the box's other tenants: median and min of 15 calls
         t = time.perf_counter()
-        h2, _, it2, _ = G.decode(llr, max_iter=max_iter, post=None)
+        h2, _, it2, v2 = G.decode(llr, max_iter=max_iter, post=None)
         th.append(time.perf_counter() - t)
     assert np.array_equal(h2, hard) and np.array_equal(it2, it)
-    out = {
-        "metric": METRIC, "value": round(B / el, 1), "unit": "codewords/s", "n_gpus": 1, "steps": reps,
-        "warmup": args.warmup, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f64", "data": "synthetic (DNA read simulator over the 272 true codewords)",
-        "config": {"workload": f"dna272-bp{max_iter}", "batch": B, "max_iter": max_iter,
-                   "mean_iters": round(float(it.mean()), 3), "genie_ok": int((hard == cw).all(axis=1).sum()),
-                   "host_api_ms_median": round(float(np.median(th)) * 1e3, 2),
-                   "host_api_ms_min": round(float(np.min(th)) * 1e3, 2),
-                   "host_api_includes": "ldpc_decode end to end: host LR (exp table for the k*ln49 alphabet, else host exp) + H2D + decode + packed hard-bit D2H + unpack"},
-    }
-    if args.cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        og = oracle.OracleGraph(synth.PCHK)
-        try:
-            threads = max(1, min(16, len(os.sched_getaffinity(0))))
-        except AttributeError:
-            threads = 1
+    out = {"workload": f"dna272-bp{max_iter}", "batch": B, "max_iter": max_iter,
+           "value": round(B / el, 1), "unit": "codewords/s", "ms_per_decode_device": round(el * 1e3, 3),
+           "mean_iters": round(float(it.mean()), 3), "genie_ok": int((hard == cw).all(axis=1).sum()),
+           "host_api_ms_median": round(float(np.median(th)) * 1e3, 3),
+           "host_api_ms_min": round(float(np.min(th)) * 1e3, 3),
+           "host_api_calls": len(th),
+           "host_api_includes": "ldpc_decode end to end: host LR (exp table for the k*ln49 alphabet, else host exp) "
+                                "+ H2D + decode + packed hard-bit D2H + unpack"}
+    if og is not None:
         t = time.perf_counter()
-        og.decode_batch(llr, max_iter, threads=threads, want_post=False)
+        rh, _, rit, rv = og.decode_batch(llr, max_iter, threads=threads, want_post=False)
         el_c = time.perf_counter() - t
+        bad = [k for k in range(B) if not (np.array_equal(rh[k], h2[k]) and rit[k] == it2[k] and bool(rv[k]) == bool(v2[k]))]
+        out["check"] = {"checked": B, "mismatches": len(bad), "first_mismatches": bad[:8],
+                        "what": "every codeword of the host-API decode vs the oracle"}
         out["cpu_baseline"] = {"value": round(B / el_c, 2), "unit": "codewords/s", "cores": threads, "kind": "port",
-                               "per_core": round(B / el_c / threads, 2),
                                "sample": f"the same 272 codewords, {max_iter} max iters, oracle on {threads} threads"}
-    print(json.dumps(out), flush=True)
+    return out
 
 
-def cpu_baseline(args, llr_fn, N, B, gpu_out):
-    """The oracle (bit-exact C restatement of dec.cpp, 'port') on the host cores,
-    on a bounded sample of the same workload -- and the check of the timed
-    GPU decode: the oracle's hard bits, iteration counts and valid flags of
-    every sampled codeword must equal the GPU's (gpu_out(start, n) -> the
-    GPU's (hard[n][N], iters[n], valid[n]) of shard rows start..start+n-1).
-    Returns (cpu_baseline dict, check dict)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    og = oracle.OracleGraph(os.path.join(ROOT, "tests", "golden", "decode_n18432_m2048_final.pchk"))
-    try:
-        threads = len(os.sched_getaffinity(0))
-    except AttributeError:
-        threads = os.cpu_count() or 1
-    avail = threads
-    threads = max(1, min(threads, 16))  # the box's CPU share for one GPU (16)
-    algo = 0 if args.algo == "bp" else 1
-    checked, bad = 0, []
+def msa_1m(args, og, threads, cw, d_cw):
+    """Config 5: min-sum (Run_MSA_Decoder_INF) with early termination on
+    `--msa-batch` codewords of BSC(p = 0.002), 1 warm-up + 2 timed decodes,
+    roofline of its dominant kernel and an oracle check of a sample."""
+    import ldpc_amd as L
+    import synth
+    G = L.Graph(synth.PCHK)
+    N = G.N
+    B, p, max_iter = args.msa_batch, 0.002, 50
+    eng = L.Engine(G, 0, "msa")
+    d_in = L.DeviceBuffer(0, B * N * 8)
+    eng.gen_bsc(d_in.at(0), L.IN_LLR, 0, B, d_cw.at(0), cw.shape[0], args.seed, p, synth.LLR_UNIT)
+    d_hard, d_iters, d_valid = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
 
-    def check(start, n, res):
-        nonlocal checked
-        rh, _, rit, rv = res
-        h, it, v = gpu_out(start, n)
-        for k in range(n):
-            if not (np.array_equal(h[k], rh[k]) and it[k] == rit[k] and bool(v[k]) == bool(rv[k])):
-                bad.append(start + k)
-        checked += n
+    def step():
+        eng.decode(d_in.at(0), L.IN_LLR, B, max_iter, d_hard.at(0), None, L.POST_LLR, d_iters.at(0), d_valid.at(0))
 
-    # calibrate with one codeword per thread, then size the sample for ~cpu_seconds
-    n0 = min(threads, B)
-    llr = llr_fn(0, n0)
+    step()
+    eng.sync()
+    eng.profile(0 if args.no_profile else 16)
+    steps = 2
     t = time.perf_counter()
-    check(0, n0, og.decode_batch(llr, args.max_iter, algo=algo, threads=threads, want_post=False))
-    t1 = time.perf_counter() - t
-    per_round = max(t1, 1e-3)
-    rounds = max(1, int(args.cpu_seconds / per_round))
-    n = max(1, min(threads * rounds, B - n0))
-    start = n0 if B > n0 else 0
-    llr = llr_fn(start, n)
-    t = time.perf_counter()
-    res = og.decode_batch(llr, args.max_iter, algo=algo, threads=threads, want_post=False)
+    for _ in range(steps):
+        step()
+    eng.sync()
     el = time.perf_counter() - t
-    check(start, n, res)
-    cb = {"value": round(n / el, 3), "unit": "codewords/s", "cores": threads, "kind": "port",
-          "per_core": round(n / el / threads, 3),
-          "sample": f"{n} codewords of the same BSC(p={args.p}) workload (indices {start}..{start + n - 1}), "
-                    f"{args.max_iter} iters, oracle/ldpc_oracle.c on {threads} host threads "
-                    f"({avail} available, capped at the box's 16-core share), {el:.1f} s"}
-    chk = {"checked": checked, "mismatches": len(bad), "first_mismatches": bad[:8],
-           "what": "hard bits, iteration counts and valid flags of the timed GPU decode vs the oracle, "
-                   "on every codeword of the cpu_baseline sample"}
-    return cb, chk
+    st = eng.stats()
+    iters = d_iters.download(np.empty(B, np.int32))
+    valid = d_valid.download(np.empty(B, np.uint8))
+    cw_iters = float(iters.sum()) * steps
+    out = {"workload": f"bsc-p{p}-{B // 1000}k-msa{max_iter}", "batch": B, "steps": steps,
+           "value": round(B * steps / el, 1), "unit": "codewords/s", "ms_per_step": round(el / steps * 1e3, 2),
+           "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 5),
+           "resident_per_pass": eng.cap, "group_tiles": eng.group_tiles, "compressed_msa": eng.msa_compressed,
+           "roofline": roofline(eng, G, st, cw_iters)}
+    if og is not None:
+        n = max(8, 4 * threads)
+
+        def llr_fn(start, k):
+            return synth.bsc_llrs(cw, start, k, seed=args.seed, p=p)
+
+        def gpu_out(start, k):
+            h = d_hard.download(np.empty((k, N), np.uint8), offset=start * N)
+            return h, iters[start:start + k], valid[start:start + k]
+
+        checked, bad, _ = oracle_check(og, llr_fn, gpu_out, 1, max_iter, [(0, n // 2), (B - n // 2, n // 2)], threads)
+        out["check"] = {"checked": checked, "mismatches": len(bad), "first_mismatches": bad[:8],
+                        "what": "hard bits, iterations, valid flags of the timed decode vs the oracle, both ends"}
+    for b in (d_in, d_hard, d_iters, d_valid):
+        b.free()
+    eng.close()
+    return out
 
 
 def main():
     args = parse()
+    cpus = host_cpus()
     if args.workload == "dna272":
-        bench_dna272(args)
-        return
+        og = _oracle().OracleGraph(os.path.join(ROOT, "tests", "golden", "decode_n18432_m2048_final.pchk")) \
+            if args.cpu_baseline else None
+        d = dna272(args, og, cpus["effective"], max_iter=args.max_iter if args.max_iter != 50 else 200)
+        out = {"metric": METRIC, "value": d.pop("value"), "unit": "codewords/s", "n_gpus": 1,
+               "steps": max(args.steps, 10), "warmup": args.warmup, "ms_per_step": d["ms_per_decode_device"],
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+               "data": "synthetic (DNA read simulator over the 272 true codewords)", "config": d}
+        for k in ("check", "cpu_baseline"):
+            if k in d:
+                out[k] = d.pop(k)
+        print(json.dumps(out), flush=True)
+        sys.exit(1 if out.get("check", {}).get("mismatches") else 0)
     import dist
-    grp = dist.Group.from_env()  # gloo control plane only: barrier + MAX/SUM of scalars
+    grp = dist.Group.from_env()  # gloo control plane only: barrier + MAX/SUM/gather of scalars
     world, rank, local = grp.world, grp.rank, grp.local
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if args.gpus != world and rank == 0:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: measuring {world} process(es); launch N "
               "ranks with python -m torch.distributed.run --nproc-per-node N", file=sys.stderr, flush=True)
@@ -214,7 +398,7 @@ def main():
     import synth
 
     G = L.Graph(synth.PCHK)
-    N, E = G.N, G.E
+    N = G.N
     if args.global_batch > 0:
         # strong scaling: this rank's contiguous shard of the global range
         # (DNA_main.cpp:629-651 Set_FrameNum's split), sizes differ by <= 1
@@ -232,10 +416,10 @@ def main():
     # fewer GPUs than ranks (rehearsals on a one-GPU box)
     dev = local % max(1, L.device_count())
     algo = args.algo
-    eng = L.Engine(G, dev, algo, chunk=args.chunk, group_tiles=args.group_tiles,
-                   nontemporal=None if args.nt < 0 else bool(args.nt), pipeline=None if args.pipe < 0 else bool(args.pipe),
-                   continuous=None if args.cont < 0 else bool(args.cont),
-                   resident=None if args.res < 0 else bool(args.res))
+    opt = lambda v: None if v < 0 else bool(v)  # noqa: E731
+    eng = L.Engine(G, dev, algo, chunk=args.chunk, group_tiles=args.group_tiles if args.group_tiles >= 0 else None,
+                   nontemporal=opt(args.nt), continuous=opt(args.cont), resident=opt(args.res),
+                   var_cpw=args.var_cpw or None)
     cw = synth.load_codewords()
     d_cw = L.DeviceBuffer(dev, cw.nbytes)
     d_cw.upload(cw)
@@ -254,7 +438,7 @@ def main():
     for _ in range(args.warmup):
         step()
     eng.sync()
-    # HIP events around a sample of the launches (<= ~1000 per kernel class)
+    # HIP events on a sample of the launches (<= ~1000 per kernel class)
     passes = -(-B // eng.cap)
     groups = -(-(-(-B // passes) // 64) // eng.group_tiles)
     est = args.steps * passes * groups * args.max_iter
@@ -279,101 +463,7 @@ def main():
         np.savez(os.path.join(args.dump_dir, f"rank{rank}.npz"), b0=b0, B=B, world=world, iters=iters, valid=valid,
                  hard=np.packbits(hard, axis=1))
 
-    # ---- roofline of the dominant kernel (algorithmic bytes) ----
     cw_iters = float(iters.sum()) * args.steps  # executed codeword-iterations (this rank)
-    M = G.M
-    if eng.msa_compressed:
-        # compressed min-sum c2v (MSA-C): the check phase
-        # reads E v->c fp64 and writes E code bytes + the (min1, min2) record
-        # planes (2 x 8 B per row; the NaN planes only when NaN occurs); the
-        # variable phase reads the codes, the records once, N LLR, writes E
-        # v->c fp64 + N/8 hard-bit ballots
-        by_kernel = {"check": 9.0 * E + 16.0 * M, "variable": 9.0 * E + 16.0 * M + 8.0 * N + N / 8.0}
-        if getattr(eng, "msa_meta", False):
-            # no per-edge codes: the check phase writes one 32-bit meta word per
-            # row, the variable phase reads it and its columns' sign bytes, and
-            # writes the sign bytes with the v2c (2 N)
-            by_kernel = {"check": 8.0 * E + 20.0 * M, "variable": 8.0 * E + 20.0 * M + 10.0 * N + N / 8.0}
-    else:
-        by_kernel = {
-            # check phase: read E v->c (d) + write E c->v (lr), fp64
-            "check": 16.0 * E,
-            # variable phase: read E lr + N LR, write E d + N/8 hard-bit ballots
-            "variable": 16.0 * E + 8.0 * N + N / 8.0,
-        }
-    if eng.pingpong:
-        # ping-pong schedule: every launch is one tile's check phase plus
-        # another tile's variable phase (k_pingpong_bp, counted as "check")
-        by_kernel["check"] = by_kernel["check"] + by_kernel["variable"]
-
-    def avg_ms(k):
-        return st[k]["ms"] / st[k]["sampled"] if st[k]["sampled"] else 0.0
-
-    dom = max(("check", "variable"), key=lambda k: avg_ms(k) * st[k]["launches"])
-    k_launch = max(1, st[dom]["launches"])
-    k_avg = avg_ms(dom)
-    bytes_per_launch = by_kernel[dom] * cw_iters / k_launch
-    achieved = bytes_per_launch / (k_avg * 1e-3) / 1e9 if k_avg > 0 else None
-    it_ms = sum(avg_ms(k) * st[k]["launches"] for k in ("check", "variable", "syndrome"))
-    iter_bytes = (32.0 * E + 10.0 * N) * cw_iters
-    # traffic: HBM bytes per codeword-iteration of this kernel from the committed
-    # rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE), scaled to this launch size
-    kname = f"k_{'check' if dom == 'check' else 'var'}_{algo}" + ("_c" if eng.msa_compressed else "")
-    if eng.pingpong:
-        kname = "k_pingpong_bp"
-    traffic, traffic_src = None, None
-    for tf in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
-        tj = json.load(open(tf))
-        if kname in tj.get("per_cw_iter", {}):
-            traffic = round(tj["per_cw_iter"][kname] * cw_iters / k_launch)
-            traffic_src = os.path.relpath(tf, ROOT)
-            break
-    if eng.tile_streams:
-        # resident pool with one stream per pool tile: the tiles' check and
-        # variable launches run concurrently, so a launch's bracket overlaps
-        # the others' and bytes per launch / its duration is no roofline.  The
-        # dominant "kernel" is the concurrent set (check + variable of every
-        # tile), its time the whole decode, bracketed by HIP events on the
-        # engine stream that every tile stream joins (ldpc_engine_wall).
-        wall_ms, runs = eng.wall()
-        set_bytes = (by_kernel["check"] + by_kernel["variable"]) * cw_iters
-        if wall_ms > 0 and runs > 0:
-            achieved = set_bytes / (wall_ms * 1e-3) / 1e9
-            k_avg = wall_ms / runs
-            bytes_per_launch = set_bytes / runs
-            it_ms = wall_ms
-        kname = f"k_check_{algo}+k_var_{algo} (concurrent tile streams)"
-        traffic, traffic_src = None, None
-        for tf in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
-            pc = json.load(open(tf)).get("per_cw_iter", {})
-            if f"k_check_{algo}" in pc and f"k_var_{algo}" in pc and runs > 0:
-                traffic = round((pc[f"k_check_{algo}"] + pc[f"k_var_{algo}"]) * cw_iters / runs)
-                traffic_src = os.path.relpath(tf, ROOT)
-                break
-    # measured ceiling of the access shape (tools/cachebench, profiles/r2/cachebench.txt): one launch per
-    # in-place pass of the check kernel's shape over a 192-224 MB working set (the resident pool's size)
-    ceiling = None if eng.msa_compressed else 6780.0  # (no measured ceiling for the compressed min-sum shapes)
-    roof = {
-        "bound": "hbm", "kernel": kname,
-        "bound_detail": "memory-side: every message byte crosses the L2 -> fabric interface once per phase (PMC "
-                        "fabric bytes = 1.02-1.04 x algorithmic, profiles/r2/pmc_traffic.json), served by HBM and "
-                        "the 256 MB Infinity Cache the resident pool is sized to; the DRAM-request counters count "
-                        "cache hits too on gfx950 (calibrated), so the cache share is not observable; no MFMA",
-        "ceiling_measured": ceiling,
-        "ceiling_source": ("tools/cachebench: in-place 72 x 512 B per wave, one launch per pass, 192-224 MB "
-                           "working set (profiles/r2/cachebench.txt)") if ceiling else None,
-        "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-        "frac_of_measured_ceiling": round(achieved / ceiling, 4) if (achieved and ceiling) else None,
-        "traffic": traffic,
-        "traffic_source": traffic_src,
-        "bytes_per_launch": round(bytes_per_launch), "avg_launch_ms": round(k_avg, 4),
-        "launch_unit": "decode (all tiles' kernels, concurrent)" if eng.tile_streams else "kernel launch",
-        "iteration_GBps": round(iter_bytes / (it_ms * 1e-3) / 1e9, 1) if it_ms > 0 else None,
-        "avg_ms": {k: round(avg_ms(k), 4) for k in st},
-        "launches": {k: v["launches"] for k, v in st.items()},
-        "sampled": {k: v["sampled"] for k, v in st.items()},
-    }
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "codewords/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(el_max / args.steps * 1e3, 3), "higher_is_better": True,
@@ -385,28 +475,57 @@ def main():
                    "max_iter": args.max_iter,
                    "algo": algo, "parallelism": f"dp{world} (contiguous codeword shards, no collective)",
                    "resident_per_pass": eng.cap, "group_tiles": eng.group_tiles, "nontemporal_d": eng.nontemporal,
-                   "two_stream": eng.pipeline, "continuous": eng.continuous, "resident_pool": eng.resident,
-                   "compressed_msa": eng.msa_compressed,
-                   "msa_meta": getattr(eng, "msa_meta", False), "syndrome_split": eng.syndrome_split,
-                   "pingpong": eng.pingpong,
+                   "continuous": eng.continuous, "resident_pool": eng.resident,
+                   "compressed_msa": eng.msa_compressed, "syndrome_split": eng.syndrome_split,
                    "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 4)},
-        "roofline": roof,
+        "roofline": roofline(eng, G, st, cw_iters),
     }
-    mismatches = 0
-    if rank == 0 and world == 1 and args.cpu_baseline:
-        def llr_fn(start, n):
-            return synth.bsc_llrs(cw, b0 + start, n, seed=args.seed, p=args.p)
 
-        def gpu_out(start, n):
-            h = d_hard.download(np.empty((n, N), np.uint8), offset=start * N)
-            return h, iters[start:start + n], valid[start:start + n]
-        out["cpu_baseline"], out["check"] = cpu_baseline(args, llr_fn, N, B, gpu_out)
-        mismatches = out["check"]["mismatches"]
+    # ---- correctness of the timed decode: every rank checks its own shard ----
+    og = _oracle().OracleGraph(os.path.join(ROOT, "tests", "golden", "decode_n18432_m2048_final.pchk"))
+    a = 0 if algo == "bp" else 1
+
+    def llr_fn(start, n):
+        return synth.bsc_llrs(cw, b0 + start, n, seed=args.seed, p=args.p)
+
+    def gpu_out(start, n):
+        h = d_hard.download(np.empty((n, N), np.uint8), offset=start * N)
+        return h, iters[start:start + n], valid[start:start + n]
+
+    threads = max(1, cpus["effective"] // max(1, local_world))
+    if world == 1 and args.cpu_baseline:
+        out["cpu_baseline"], (checked, bad) = cpu_baseline(args, og, llr_fn, B, gpu_out, cpus)
+    else:
+        n = min(B, max(2, args.check_per_thread * threads))
+        checked, bad, _ = oracle_check(og, llr_fn, gpu_out, a, args.max_iter, [(0, n - n // 2), (B - n // 2, n // 2)],
+                                       threads)
+    per = grp.gather({"rank": rank, "b0": b0, "B": B, "checked": checked, "mismatches": len(bad),
+                      "first_mismatches": [b0 + k for k in bad[:4]], "threads": threads})
+    out["check"] = {"checked": sum(p["checked"] for p in per), "mismatches": sum(p["mismatches"] for p in per),
+                    "per_rank": per,
+                    "what": "hard bits, iteration counts and valid flags of the timed GPU decode vs the oracle, on "
+                            "a sample of every rank's own shard (N = 1: the cpu_baseline sample)"}
+    mismatches = out["check"]["mismatches"]
+
+    # ---- secondary legs (N = 1): config 2 and config 5, each checked ----
+    if world == 1 and args.secondary and args.global_batch == 0 and algo == "bp":
+        for b in (d_in, d_hard, d_iters, d_valid):
+            b.free()
+        eng.close()
+        sec = {"note": "driver-timed after the headline region; not part of value / ms_per_step"}
+        t = time.perf_counter()
+        sec["config5_msa_1m"] = msa_1m(args, og, cpus["effective"], cw, d_cw)
+        sec["config5_msa_1m"]["leg_wall_s"] = round(time.perf_counter() - t, 2)
+        t = time.perf_counter()
+        sec["config2_dna272"] = dna272(args, og, cpus["effective"])
+        sec["config2_dna272"]["leg_wall_s"] = round(time.perf_counter() - t, 2)
+        out["secondary"] = sec
+        mismatches += sum(v.get("check", {}).get("mismatches", 0) for v in sec.values() if isinstance(v, dict))
     if rank == 0:
         print(json.dumps(out), flush=True)
     grp.close()
     if mismatches:
-        print(f"bench.py: {mismatches} codewords of the timed decode differ from the oracle", file=sys.stderr)
+        print(f"bench.py: {mismatches} codewords of the timed decodes differ from the oracle", file=sys.stderr)
         sys.exit(1)
 
 

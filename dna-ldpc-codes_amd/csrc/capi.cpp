@@ -35,8 +35,9 @@ using ldpc::set_error;
 // (the 272-codeword DNA batch: 248k cw/s grouped vs 194k through the
 // resident pool); larger ones use the engine's own pool
 constexpr int64_t kExplicitPoolMax = 1024;
-constexpr int64_t kXferChunk = 4096;  // codewords per PCIe chunk (at least)
-constexpr int64_t kSmallXfer = 0;  // ... and for shards of <= kExplicitPoolMax (LDPC_SMALL_XFER; 0: one chunk -- A/B on the DNA batch: 128, 192 and one chunk within noise, 64 slower)
+constexpr int64_t kXferChunk = 4096;  // codewords per PCIe chunk (at least); shards of <= kExplicitPoolMax
+                                      // cross in one chunk (A/B on the DNA batch: chunks of 128 or 192
+                                      // within noise of one, 64 slower)
 
 namespace {
 
@@ -164,6 +165,7 @@ struct Slot {
     std::unique_ptr<Engine> eng;
     int device = 0, algo = 0;
     int64_t pool = 0, xfer = 0;
+    ldpc_schedule sched{};  // resolved (ldpc::resolve_schedule): the engine's schedule
     hipStream_t copy = nullptr, copy_out = nullptr;  // H2D / D2H streams (the engine computes on its own)
     hipEvent_t ev_h2d[2] = {}, ev_dec[2] = {}, ev_d2h[2] = {};
     double* h_in[2] = {};
@@ -212,13 +214,15 @@ struct Slot {
     }
 };
 
-int make_slot(const HostGraph* g, int device, int algo, int64_t pool, int64_t xfer, std::unique_ptr<Slot>& out)
+int make_slot(const HostGraph* g, int device, int algo, int64_t pool, int64_t xfer, const ldpc_schedule& sched,
+              std::unique_ptr<Slot>& out)
 {
     auto s = std::make_unique<Slot>();
     s->device = device;
     s->algo = algo;
+    s->sched = sched;
     s->eng = std::make_unique<Engine>();
-    int rc = s->eng->init(g, device, algo, pool);
+    int rc = s->eng->init(g, device, algo, pool, &sched);
     if (rc) return rc;
     s->pool = pool;
     s->xfer = xfer;
@@ -275,13 +279,14 @@ struct ldpc_graph {
     // at least `xfer` codewords per chunk
     // (small: any small-batch pool of at least `pool` lanes will do -- the
     // extra tiles stay empty -- so calls of varying small sizes share one)
-    std::unique_ptr<Slot> take(int device, int algo, int64_t pool, int64_t xfer, bool small)
+    std::unique_ptr<Slot> take(int device, int algo, int64_t pool, int64_t xfer, bool small, const ldpc_schedule& sched)
     {
         std::lock_guard<std::mutex> lk(mu);
         for (size_t i = 0; i < free_slots.size(); i++) {
             auto& s = free_slots[i];
             const bool pool_ok = small ? (s->pool >= pool && s->pool <= kExplicitPoolMax) : s->pool == pool;
-            if (s->device == device && s->algo == algo && pool_ok && s->xfer >= xfer) {
+            if (s->device == device && s->algo == algo && pool_ok && s->xfer >= xfer &&
+                std::memcmp(&s->sched, &sched, sizeof(sched)) == 0) {
                 auto r = std::move(s);
                 free_slots.erase(free_slots.begin() + (long)i);
                 return r;
@@ -406,7 +411,7 @@ int ldpc_graph_info(const ldpc_graph* g, int32_t* M, int32_t* N, int64_t* E, int
 int ldpc_graph_blocks(const ldpc_graph* g, int32_t* Q, int32_t* row_blocks, int32_t* col_blocks, int32_t* col_block)
 {
     if (!g) { set_error("null graph"); return LDPC_ERR_ARG; }
-    const ldpc::XrLayout* L = ldpc::xr_layout_of(g->h);
+    const ldpc::BlockLayout* L = ldpc::block_layout_of(g->h);
     if (Q) *Q = L ? L->Q : 0;
     if (row_blocks) *row_blocks = L ? L->GA : 0;
     if (col_blocks) *col_blocks = L ? L->RB : 0;
@@ -461,11 +466,11 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
     for (int i = 0; i < ndev; i++) devs.push_back(o.devices ? o.devices[i] : i);
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
     const int host_threads = o.host_threads > 0 ? o.host_threads : std::min(16, std::max(1, hw / ndev));
-    const char* tev = std::getenv("LDPC_LR_TABLE");
-    const bool lr_table = !(tev && *tev && std::atoi(tev) == 0);
-    const char* xev = std::getenv("LDPC_SMALL_XFER");
-    const int64_t small_xfer = (xev && *xev) ? (std::atoll(xev) + 63) / 64 * 64 : kSmallXfer;
-    const char* pev = std::getenv("LDPC_API_TIMING");  // debug: host-leg split to stderr
+    const ldpc_schedule sched = ldpc::resolve_schedule(o.schedule);
+    const bool lr_table = ldpc::sched_flag(sched, LDPC_SCHED_LR_TABLE);
+    // the only environment variable the library reads: a debug print of the
+    // host-leg split (never changes what is computed)
+    const char* pev = std::getenv("LDPC_API_TIMING");
     const bool api_timing = pev && *pev && std::atoi(pev) != 0;
     auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const size_t N = (size_t)g->h.N;
@@ -484,14 +489,10 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
         // PCIe in double-buffered chunks of `xfer`.
         const int64_t sh64 = (shard + 63) / 64 * 64;
         const int64_t pool = o.chunk > 0 ? o.chunk : (shard <= kExplicitPoolMax ? sh64 : 0);
-        // small shards (the DNA batch) cross in chunks of kSmallXfer codewords,
-        // so the host work on one chunk overlaps the decode of the one before
-        const int64_t xfer = (o.chunk <= 0 && shard <= kExplicitPoolMax && small_xfer > 0)
-                                 ? std::min<int64_t>(sh64, small_xfer)
-                                 : std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool + 63) / 64 * 64));
-        std::unique_ptr<Slot> slot = g->take(dev, algo, pool, xfer, o.chunk <= 0 && pool > 0);
+        const int64_t xfer = std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool + 63) / 64 * 64));
+        std::unique_ptr<Slot> slot = g->take(dev, algo, pool, xfer, o.chunk <= 0 && pool > 0, sched);
         int rc = LDPC_OK;
-        if (!slot) rc = make_slot(&g->h, dev, algo, pool, xfer, slot);
+        if (!slot) rc = make_slot(&g->h, dev, algo, pool, xfer, sched, slot);
         if (!rc && post_out) rc = slot->want_post(N);
         if (rc) { rcs[di] = rc; msgs[di] = ldpc::last_error(); return; }
         if (!slot->workers || slot->workers->size() != host_threads) slot->workers = std::make_unique<Workers>(host_threads);
@@ -673,13 +674,12 @@ int ldpc_engine_set_params(ldpc_engine* e, int32_t msa_precision, double msa_ste
 }
 
 ldpc_engine* ldpc_engine_create_ex(const ldpc_graph* g, int32_t device, int32_t algo, int64_t chunk,
-                                   int64_t group_tiles, int32_t flags_set, int32_t flags, int* err)
+                                   const ldpc_schedule* schedule, int* err)
 {
-    auto bit = [&](int b) { return ((flags_set >> b) & 1) ? ((flags >> b) & 1) : -1; };
     if (!g) { set_error("null graph"); fail(LDPC_ERR_ARG, err); return nullptr; }
     auto e = std::make_unique<ldpc_engine>();
     e->e = std::make_unique<Engine>();
-    int rc = e->e->init(&g->h, device, algo, chunk, group_tiles, bit(0), bit(1), bit(2), bit(3), bit(5));
+    int rc = e->e->init(&g->h, device, algo, chunk, schedule);
     if (rc) { fail(rc, err); return nullptr; }
     if (err) *err = LDPC_OK;
     return e.release();
@@ -687,7 +687,7 @@ ldpc_engine* ldpc_engine_create_ex(const ldpc_graph* g, int32_t device, int32_t 
 
 ldpc_engine* ldpc_engine_create(const ldpc_graph* g, int32_t device, int32_t algo, int64_t chunk, int* err)
 {
-    return ldpc_engine_create_ex(g, device, algo, chunk, -1, 0, 0, err);
+    return ldpc_engine_create_ex(g, device, algo, chunk, nullptr, err);
 }
 
 int ldpc_engine_info(ldpc_engine* e, int64_t* cap, int64_t* group_tiles, int32_t* flags)
@@ -695,11 +695,7 @@ int ldpc_engine_info(ldpc_engine* e, int64_t* cap, int64_t* group_tiles, int32_t
     if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
     if (cap) *cap = e->e->cap;
     if (group_tiles) *group_tiles = e->e->group_tiles;
-    if (flags) *flags = (e->e->nt_d ? 1 : 0) | (e->e->pipe ? 2 : 0) | (e->e->lr_csc ? 4 : 0) | (e->e->cont ? 8 : 0) |
-                        (e->e->msa_c ? 16 : 0) | (e->e->res ? 32 : 0) | (e->e->syn_split ? 64 : 0) |
-                        (e->e->syn_fused ? 128 : 0) | (e->e->res && e->e->tile_streams ? 256 : 0) |
-                        (e->e->res && e->e->pingpong ? 512 : 0) | (e->e->xr ? 1024 : 0) |
-                        (e->e->msa_meta ? 2048 : 0);
+    if (flags) *flags = e->e->flags();
     return LDPC_OK;
 }
 
@@ -736,19 +732,7 @@ int ldpc_engine_profile(ldpc_engine* e, int32_t stride)
     int rc = e->e->collect_stats();
     if (rc) return rc;
     for (int c = 0; c < ldpc::K_NCLASS; c++) { e->e->launches[c] = 0; e->e->ms[c] = 0; e->e->sampled[c] = 0; }
-    e->e->wall_ms = 0;
-    e->e->wall_runs = 0;
     e->e->profile_stride = stride > 0 ? stride : 0;
-    return LDPC_OK;
-}
-
-int ldpc_engine_wall(ldpc_engine* e, double* ms, int64_t* runs)
-{
-    if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
-    int rc = e->e->collect_stats();
-    if (rc) return rc;
-    if (ms) *ms = e->e->wall_ms;
-    if (runs) *runs = e->e->wall_runs;
     return LDPC_OK;
 }
 

@@ -487,13 +487,13 @@ bool check_col_blocks(const HostGraph& g, const std::vector<int32_t>& cls, int32
 
 }  // namespace
 
-bool find_xr_layout(const HostGraph& g, XrLayout& L)
+bool find_block_layout(const HostGraph& g, BlockLayout& L)
 {
-    if (!g.regular_dv || !g.regular_dc || g.dv_max < 1 || g.dv_max > 8 || g.dc_max < 2) return false;
+    if (!g.regular_dv || !g.regular_dc || g.dv_max < 1 || g.dc_max < 2) return false;
     const int32_t GA = g.dv_max, RB = g.dc_max;
     if (g.M % GA != 0) return false;
     const int32_t Q = g.M / GA;
-    if (Q % 64 != 0 || Q > 256 || (int64_t)g.N != (int64_t)RB * Q) return false;
+    if ((int64_t)g.N != (int64_t)RB * Q) return false;
     // row blocks: rows a*Q .. a*Q+Q-1 cover every column exactly once
     std::vector<int32_t> seen((size_t)g.N, -1);
     for (int32_t i = 0; i < g.M; i++)
@@ -529,40 +529,28 @@ bool find_xr_layout(const HostGraph& g, XrLayout& L)
         if (!check_col_blocks(g, cls, RB, Q)) return false;
     }
     // position of each column inside its block (ascending column index)
-    std::vector<int32_t> jp((size_t)g.N), fill((size_t)RB, 0);
-    for (int32_t j = 0; j < g.N; j++) jp[(size_t)j] = fill[(size_t)cls[(size_t)j]]++;
+    std::vector<int32_t> fill((size_t)RB, 0);
     L.Q = Q;
     L.GA = GA;
     L.RB = RB;
-    const int32_t RW = (RB + 3) / 4;
-    L.jpb.assign((size_t)GA * RB * Q, 0);
-    L.ord4.assign((size_t)GA * RW * Q, 0);
-    L.inv8.assign((size_t)RB * Q, 0);
     L.col_orig.assign((size_t)RB * Q, 0);
-    for (int32_t i = 0; i < g.M; i++) {
-        const int32_t a = i / Q, r = i % Q;
-        for (int32_t e = g.row_ptr[(size_t)i]; e < g.row_ptr[(size_t)i + 1]; e++) {
-            const int32_t j = g.col_idx[(size_t)e], b = cls[(size_t)j];
-            const int32_t rank = e - g.row_ptr[(size_t)i];  // position in the row's column order
-            L.jpb[((size_t)a * RB + b) * Q + r] = (uint8_t)jp[(size_t)j];
-            L.ord4[((size_t)a * RW + rank / 4) * Q + r] |= (uint32_t)b << (8 * (rank % 4));
-            L.inv8[(size_t)b * Q + jp[(size_t)j]] |= (uint64_t)r << (8 * a);
-            L.col_orig[(size_t)b * Q + jp[(size_t)j]] = j;
-        }
+    for (int32_t j = 0; j < g.N; j++) {
+        const int32_t b = cls[(size_t)j];
+        L.col_orig[(size_t)b * Q + fill[(size_t)b]++] = j;
     }
     return true;
 }
 
-const XrLayout* xr_layout_of(const HostGraph& g)
+const BlockLayout* block_layout_of(const HostGraph& g)
 {
     static std::mutex mu;
     std::lock_guard<std::mutex> lk(mu);
-    if (g.xr_state == 0) {
-        auto L = std::make_shared<XrLayout>();
-        g.xr_state = find_xr_layout(g, *L) ? 1 : -1;
-        if (g.xr_state > 0) g.xr_cache = L;
+    if (g.blk_state == 0) {
+        auto L = std::make_shared<BlockLayout>();
+        g.blk_state = find_block_layout(g, *L) ? 1 : -1;
+        if (g.blk_state > 0) g.blk_cache = L;
     }
-    return g.xr_state > 0 ? g.xr_cache.get() : nullptr;
+    return g.blk_state > 0 ? g.blk_cache.get() : nullptr;
 }
 
 }  // namespace ldpc

@@ -9,7 +9,7 @@
 
 namespace ldpc {
 
-struct XrLayout;
+struct BlockLayout;
 
 // Sparse GF(2) parity-check matrix laid out once as flat edge arrays.
 // Replaces the reference's doubly-linked mod2sparse lists (mod2sparse.h:42-93):
@@ -23,9 +23,9 @@ struct HostGraph {
     std::vector<int32_t> row_ptr, col_idx, col_ptr, col_edge, edge_row;
     int32_t dv_max = 0, dc_max = 0;
     bool regular_dv = true, regular_dc = true;
-    // block structure (xr_layout_of), found once per graph
-    mutable int xr_state = 0;  // 0 not looked for, 1 found, -1 none
-    mutable std::shared_ptr<XrLayout> xr_cache;
+    // block structure (block_layout_of), found once per graph
+    mutable int blk_state = 0;  // 0 not looked for, 1 found, -1 none
+    mutable std::shared_ptr<BlockLayout> blk_cache;
 };
 
 // Parse a .pchk (rcode.cpp:54-85 / mod2sparse.cpp:381-427).  Returns an
@@ -57,29 +57,20 @@ int save_alist(const HostGraph& g, const std::string& path, std::string* msg);
 int build_rs_ldpc(int s, int rho, int gamma, HostGraph& g, std::vector<int>* gen_poly,
                   std::vector<int>* coset, std::string* msg);
 
-// Block structure of array (RS / quasi-cyclic) codes, for the XCD-resident
-// decoder (kernels_xr.hpp): rows in GA = dv contiguous blocks of Q, columns in
-// RB = dc blocks of Q, every (row block, column block) submatrix a Q x Q
-// permutation.  Column b*Q + jp of the block layout is the jp-th column (in
-// ascending index) of column block b.
-struct XrLayout {
+// Block structure of array (RS / quasi-cyclic) codes (ldpc_graph_blocks):
+// rows in GA = dv contiguous blocks of Q, columns in RB = dc blocks of Q,
+// every (row block, column block) submatrix a Q x Q permutation.
+struct BlockLayout {
     int32_t Q = 0, GA = 0, RB = 0;
-    // [GA][RB][Q]: row r of row block a -> jp, the position in column block b
-    // of the row's column in that block
-    std::vector<uint8_t> jpb;
-    // [GA][(RB+3)/4][Q]: byte k%4 of word k/4 = the column block of the row's
-    // k-th edge (CSR order = ascending column, the reference's row order)
-    std::vector<uint32_t> ord4;
-    std::vector<uint64_t> inv8;      // [RB][Q]: byte a = row (within block a) of column (b, jp)
-    std::vector<int32_t> col_orig;   // [RB][Q]: column index
+    std::vector<int32_t> col_orig;  // [RB][Q]: column index of position jp of column block b (ascending)
 };
 
 // Column blocks: contiguous blocks of Q, else the RS-LDPC(log2 Q, dc, dv)
 // code's blocks when H is that code with permuted columns.  False when H has
-// no such structure (or dv > 8, Q not a multiple of 64, Q > 256).
-bool find_xr_layout(const HostGraph& g, XrLayout& L);
+// no such structure.
+bool find_block_layout(const HostGraph& g, BlockLayout& L);
 
-// find_xr_layout once per graph (thread-safe); nullptr when H has no such structure
-const XrLayout* xr_layout_of(const HostGraph& g);
+// find_block_layout once per graph (thread-safe); nullptr when H has no such structure
+const BlockLayout* block_layout_of(const HostGraph& g);
 
 }  // namespace ldpc

@@ -14,9 +14,8 @@ struct Refill {
     const int64_t* lane_b;  // [tile*64] codeword index held by each lane
     const double* in;       // [B][N] input (LLR or LR)
     int in_is_llr;
-    // resident pool (engine `res`, k_var_m only): outputs of the codewords
-    // that finished at this step's syndrome, written before their lanes are
-    // refilled (fin == nullptr: the syndrome kernel wrote them)
+    // continuous mode: outputs of the codewords that finished at this step's
+    // syndrome, written by the variable kernel before their lanes are refilled
     const uint64_t* fin;    // [tile] finished lanes
     const int64_t* fin_b;   // [tile*64] their codeword index
     const int32_t* fin_n;   // [tile*64] their iteration count
@@ -54,18 +53,15 @@ constexpr int kOccTileShift = 40;
 constexpr unsigned long long kOccMask = (1ull << kOccTileShift) - 1ull;
 
 struct ContOut {
-    uint8_t* hard;    // [B][N]
-    double* post;     // [B][N] or nullptr
-    int32_t* iters;   // [B]
-    uint8_t* valid;   // [B]
-    const double* post_t;  // [tile][N][64] per-iteration posterior (when post)
-    const double* prior;   // [tile][N][64]
-    int algo_msa, post_ratio;
+    int32_t* iters;   // [B] the decode's iteration-count output
+    uint8_t* valid;   // [B] its valid-flag output
 };
 
-// Resident pool: the syndrome of the previous variable phase is computed by
-// the check kernel (each wave its row's parity) and the last block of a tile
-// to finish runs the lane bookkeeping (k_check_bp / k_check_msa with SYN).
+// Continuous-mode syndrome step: the parity of every row over the previous
+// variable phase's ballots, computed by the resident pool's check kernel
+// (each wave its row, k_check_bp / k_check_msa with RES) or by
+// k_syndrome_split (grouped schedule); the last block of a tile to finish runs
+// the lane bookkeeping.
 struct ResStep {
     const uint64_t* hard;        // [tile][N] ballots
     const int32_t* col_idx;      // [E] CSR column of each edge (regular rows)
@@ -76,54 +72,7 @@ struct ResStep {
     int32_t* fin_n;              // [tile*64]
     int32_t N, max_iter;
     ContState cs;
-    ContOut co;                  // iters / valid (hard / post are written by k_var_m)
-};
-
-// XCD-resident BP decoder (kernels_xr.hpp)
-constexpr uint32_t XR_DEAD = 0xFFFFFFFFu;
-enum : unsigned long long { XR_LIVE = 1, XR_FIN = 2, XR_FRESH = 4 };
-// packed slot state: codeword (40 bits, all ones = none) | iterations << 40 | mode << 56
-constexpr unsigned long long XR_CW_MASK = (1ull << 40) - 1, XR_NO_CW = XR_CW_MASK;
-__host__ __device__ constexpr unsigned long long xr_state(unsigned long long cw, unsigned long long n,
-                                                          unsigned long long mode)
-{
-    return (cw & XR_CW_MASK) | ((n & 0xffffull) << 40) | (mode << 56);
-}
-
-// one slot's control words (128 B apart); only atomics touch them
-struct XrCtl {
-    unsigned long long ctl;    // (phase << 32) | tasks claimed
-    unsigned long long done;   // tasks finished since the decode began (monotone)
-    unsigned long long unsat;  // the last check phase that found an unsatisfied row (atomicMax)
-    unsigned long long state;  // xr_state(codeword held, its iterations, variable-phase mode)
-    unsigned long long fin;    // XR_FIN: xr_state(finished codeword, its iterations, 0)
-    unsigned long long pad[11];
-};
-
-struct XrArgs {
-    const uint8_t* jpb;       // [GA][RB][Q]
-    const uint32_t* ord4;     // [GA][(RB+3)/4][Q]
-    const uint64_t* inv8;     // [RB][Q]
-    const int32_t* col_orig;  // [RB][Q]
-    int32_t Q, N;
-    int64_t E;
-    double* msg;              // [S][E]
-    double* prior;            // [S][N]
-    double* post;             // [S][N] per-iteration posterior, or nullptr
-    uint64_t* hb;             // [S][N/64]
-    XrCtl* ctl;               // [S]
-    int32_t K, nxcd;          // slots per XCD, XCDs
-    const double* in;         // [B][N]
-    int32_t in_is_llr;
-    int32_t max_iter;
-    int64_t B;
-    unsigned long long* next_b;
-    uint8_t* hard_out;        // [B][N]
-    double* post_out;         // [B][N] or nullptr
-    int32_t post_ratio;
-    int32_t* iters_out;
-    uint8_t* valid_out;
-    unsigned long long* prof;  // [grid][8] or nullptr (LDPC_XR_PROF)
+    ContOut co;                  // iters / valid (hard / post are written by the variable kernel)
 };
 
 }  // namespace dev

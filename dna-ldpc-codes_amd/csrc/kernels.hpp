@@ -83,7 +83,7 @@ struct Msg<true> {
     using out = double*;
 };
 
-// Whole-line lane policy (full_lanes bit 0): a lane with no codeword, or a
+// Whole-line lane policy: a lane with no codeword, or a
 // finished one, still runs when its 16-lane group -- one 128-byte line of
 // every 512-byte message segment -- holds a lane that is being decoded, so
 // message stores cover whole lines; lines without one are neither read nor
@@ -177,30 +177,6 @@ __device__ __forceinline__ void cont_lanes(int64_t t, uint64_t occ, uint64_t U, 
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             if (t == 0 && cs.occ_clear) *cs.occ_clear = 0ull;
-        }
-    }
-}
-
-// The finished codewords' outputs (hard bits of this step, posterior), all
-// threads of the block.
-__device__ __forceinline__ void cont_outputs(int64_t t, uint64_t F, const uint64_t* __restrict__ h, int32_t N,
-                                             const ContOut& co, const int64_t* s_b, const int32_t* s_n)
-{
-    for (int32_t j = threadIdx.x; j < N; j += blockDim.x) {
-        const uint64_t wj = h[j];
-        for (uint64_t f = F; f; f &= f - 1) {
-            const int l = __builtin_ctzll(f);
-            const size_t ob = (size_t)s_b[l] * N + j;
-            co.hard[ob] = (uint8_t)((wj >> l) & 1ull);
-            if (co.post) {
-                const size_t pj = ((size_t)t * N + j) * TILE + l;
-                const double pv = s_n[l] > 0 ? co.post_t[pj] : co.prior[pj];
-                if (co.algo_msa) co.post[ob] = pv;
-                else {
-                    const double P = __builtin_isnan(pv) ? 1.0 : pv;
-                    co.post[ob] = co.post_ratio ? P : log(P);
-                }
-            }
         }
     }
 }
@@ -385,8 +361,6 @@ __global__ __launch_bounds__(1024) void k_syndrome(const uint64_t* __restrict__ 
 // -> identical values), which keeps the kernel at 2 waves/SIMD.
 // grid (ceil(M/4), tiles), block 256: one wave per (row, tile).
 // ---------------------------------------------------------------------------
-// c2v scratch: CSR order (row-contiguous) or CSC order (column-contiguous,
-// position pos[e]) so the variable phase reads each column contiguously
 template <int DC, bool NT, bool INPLACE>
 __device__ __forceinline__ void check_bp_load(double (&x)[DC], typename Msg<INPLACE>::in src)
 {
@@ -394,9 +368,9 @@ __device__ __forceinline__ void check_bp_load(double (&x)[DC], typename Msg<INPL
     for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
 }
 
-template <int DC, bool CSCL, bool INPLACE>
-__device__ __forceinline__ void check_bp_compute(const double (&x)[DC], typename Msg<INPLACE>::out dst,
-                                                 const int32_t* __restrict__ prow, int32_t row)
+// dst: the row's first c2v message (CSR order, row-contiguous)
+template <int DC, bool INPLACE>
+__device__ __forceinline__ void check_bp_compute(const double (&x)[DC], typename Msg<INPLACE>::out dst)
 {
     constexpr int SEG = 8;
     constexpr int NSEG = (DC + SEG - 1) / SEG;
@@ -425,55 +399,45 @@ __device__ __forceinline__ void check_bp_compute(const double (&x)[DC], typename
             const int k = g * SEG + i;
             if (k < DC) {
                 const double tt = pk[i] * s;
-                const size_t p = CSCL ? (size_t)prow[k] : (size_t)row * DC + k;
-                dst[p * TILE] = (1.0 + tt) / (1.0 - tt);
+                dst[(size_t)k * TILE] = (1.0 + tt) / (1.0 - tt);
                 s = s * x[k];
             }
         }
     }
 }
 
-template <int DC, bool NT, bool CSCL, bool INPLACE>
-__device__ __forceinline__ void check_bp_row(typename Msg<INPLACE>::in src, typename Msg<INPLACE>::out dst,
-                                             const int32_t* __restrict__ prow, int32_t row)
-{
-    double x[DC];
-    check_bp_load<DC, NT, INPLACE>(x, src);
-    check_bp_compute<DC, CSCL, INPLACE>(x, dst, prow, row);
-}
-
-// SYN (resident pool, ResStep): the lanes run are the tile's occupied ones,
-// every wave also takes its row's parity over the previous variable phase's
-// ballots, and every block ends in res_arrive (no early exit).
-// INPLACE: lr == dmsg (resident pool), see Msg.
+// RES (resident pool, ResStep): messages in place (lr == dmsg, see Msg), the
+// lanes run are the tile's occupied ones, every wave also takes its row's
+// parity over the previous variable phase's ballots, and every block ends in
+// res_arrive (no early exit).
 // Block rb of nrb row blocks of tile t; lr_t = the tile's c2v messages.
-template <int DC, bool NT, bool CSCL, bool SYN, bool INPLACE>
-__device__ __forceinline__ void check_bp_block(typename Msg<INPLACE>::in dmsg, typename Msg<INPLACE>::out lr_t,
-                                               const uint64_t* __restrict__ active, const int32_t* __restrict__ pos,
-                                               int32_t M, int64_t E, int64_t t, uint32_t rb, uint32_t nrb,
-                                               int full_lanes, const ResStep& rs)
+template <int DC, bool NT, bool RES>
+__device__ __forceinline__ void check_bp_block(typename Msg<RES>::in dmsg, typename Msg<RES>::out lr_t,
+                                               const uint64_t* __restrict__ active, int32_t M, int64_t E,
+                                               int64_t t, uint32_t rb, uint32_t nrb, const ResStep& rs)
 {
     const int lane = lane_id();
     const int32_t row = (int32_t)rb * 4 + wave_id();
-    const uint64_t act = SYN ? rs.cs.occupied[t] : active[t];
-    // full_lanes: converged / empty lanes of an active tile run along on their
-    // stale state so every c2v store covers whole lines (their values are never read)
-    const bool run = row < M && ((full_lanes & 1) ? line_occupied(act, lane) : ((act >> lane) & 1ull));
-    if constexpr (!SYN) {
-        if (!run) return;
-    }
+    const uint64_t act = RES ? rs.cs.occupied[t] : active[t];
     const auto src = dmsg + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
-    if constexpr (!SYN) {
-        check_bp_row<DC, NT, CSCL, INPLACE>(src, lr_t + lane, pos + (size_t)row * DC, row);
+    const auto dst = lr_t + (size_t)row * DC * TILE + lane;
+    if constexpr (!RES) {
+        // whole-line policy: converged / empty lanes of an active tile run
+        // along on their stale state so every c2v store covers whole lines
+        // (their values are never read)
+        if (!(row < M && line_occupied(act, lane))) return;
+        double x[DC];
+        check_bp_load<DC, NT, false>(x, src);
+        check_bp_compute<DC, false>(x, dst);
     } else {
         // Issue order inside one wave-uniform arm: the row's column indices,
         // its DC message loads, the parity's ballot gathers (which need the
         // indices), the arithmetic, then the XOR reduction -- the gathers'
         // latency hides behind the messages instead of preceding them.  All
-        // lanes of an occupied tile run (whole-line stores whatever
-        // full_lanes says; unoccupied lanes' values are never read): a
-        // lane-masked arm, or a join between the loads and their uses, makes
-        // the compiler wait for every outstanding load there.
+        // lanes of an occupied tile run (whole-line stores; unoccupied lanes'
+        // values are never read): a lane-masked arm, or a join between the
+        // loads and their uses, makes the compiler wait for every outstanding
+        // load there.
         static_assert(DC <= 2 * TILE, "row parity: two gathers per lane");
         const bool occ_l = (act >> lane) & 1ull;
         // the lane state for res_arrive's bookkeeping (the tile's last block,
@@ -486,7 +450,7 @@ __device__ __forceinline__ void check_bp_block(typename Msg<INPLACE>::in dmsg, t
             const int32_t c0 = cols[lane < DC ? lane : DC - 1];
             const int32_t c1 = cols[TILE + lane < DC ? TILE + lane : DC - 1];
             double x[DC];
-            check_bp_load<DC, NT, INPLACE>(x, src);
+            check_bp_load<DC, NT, true>(x, src);
             // opaque copies: the gather addresses (and the wait for the
             // index loads) stay behind the message loads
             int32_t d0 = c0, d1 = c1;
@@ -494,7 +458,7 @@ __device__ __forceinline__ void check_bp_block(typename Msg<INPLACE>::in dmsg, t
             const uint64_t* __restrict__ h = rs.hard + (size_t)t * rs.N;
             const uint64_t g0 = h[d0];
             const uint64_t g1 = h[d1];
-            check_bp_compute<DC, CSCL, INPLACE>(x, lr_t + lane, pos + (size_t)row * DC, row);
+            check_bp_compute<DC, true>(x, dst);
             uint64_t p = (lane < DC ? g0 : 0ull) ^ (TILE + lane < DC ? g1 : 0ull);
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) p ^= shfl_xor_u64(p, off);
@@ -510,19 +474,17 @@ __device__ __forceinline__ void check_bp_block(typename Msg<INPLACE>::in dmsg, t
 // the refill (Init_Belief_Propagation dec.cpp:608-629 + the stored d of
 // dec.cpp:652) -- gathered from the tile's [N][64] prior instead of read from
 // E stored copies; then k_check_bp's arithmetic.  Same grid as k_check_bp.
-template <int DC, bool CSCL>
+template <int DC>
 __global__ __launch_bounds__(256, 2) void k_check_bp_first(const double* __restrict__ prior,
                                                            const int32_t* __restrict__ col_idx,
                                                            double* __restrict__ lr, const uint64_t* __restrict__ active,
-                                                           const int32_t* __restrict__ pos, int32_t M, int32_t N,
-                                                           int64_t E, int64_t t0, int full_lanes)
+                                                           int32_t M, int32_t N, int64_t E, int64_t t0)
 {
     const int lane = lane_id();
     const int32_t row = (int32_t)blockIdx.x * 4 + wave_id();
     const int64_t t = t0 + blockIdx.y;
     const uint64_t act = active[t];
-    const bool run = row < M && ((full_lanes & 1) ? line_occupied(act, lane) : ((act >> lane) & 1ull));
-    if (!run) return;
+    if (!(row < M && line_occupied(act, lane))) return;
     const double* __restrict__ pt = prior + (size_t)t * N * TILE + lane;
     const int32_t* __restrict__ cols = col_idx + (size_t)row * DC;
     double x[DC];
@@ -530,17 +492,18 @@ __global__ __launch_bounds__(256, 2) void k_check_bp_first(const double* __restr
     for (int k = 0; k < DC; ++k) x[k] = pt[(size_t)cols[k] * TILE];
 #pragma unroll
     for (int k = 0; k < DC; ++k) x[k] = 1.0 - 2.0 / (1.0 + x[k]);
-    check_bp_compute<DC, CSCL, false>(x, lr + (size_t)blockIdx.y * E * TILE + lane, pos + (size_t)row * DC, row);
+    check_bp_compute<DC, false>(x, lr + ((size_t)blockIdx.y * E + (size_t)row * DC) * TILE + lane);
 }
 
-template <int DC, bool NT, bool CSCL, bool SYN, bool INPLACE>
-__global__ __launch_bounds__(256, 2) void k_check_bp(typename Msg<INPLACE>::in dmsg, typename Msg<INPLACE>::out lr,
-                                                     const uint64_t* __restrict__ active,
-                                                     const int32_t* __restrict__ pos, int32_t M, int64_t E,
-                                                     int64_t t0, int full_lanes, ResStep rs)
+// grid (ceil(M/4), tiles t0 .. t0+gridDim.y-1); lr: the group's c2v scratch
+// ([t - t0][E][64]), or with RES the pool's messages themselves (in place).
+template <int DC, bool NT, bool RES>
+__global__ __launch_bounds__(256, 2) void k_check_bp(typename Msg<RES>::in dmsg, typename Msg<RES>::out lr,
+                                                     const uint64_t* __restrict__ active, int32_t M, int64_t E,
+                                                     int64_t t0, ResStep rs)
 {
-    check_bp_block<DC, NT, CSCL, SYN, INPLACE>(dmsg, lr + (size_t)blockIdx.y * E * TILE, active, pos, M, E,
-                                               t0 + blockIdx.y, blockIdx.x, gridDim.x, full_lanes, rs);
+    check_bp_block<DC, NT, RES>(dmsg, lr + (size_t)blockIdx.y * E * TILE, active, M, E, t0 + blockIdx.y, blockIdx.x,
+                                gridDim.x, rs);
 }
 
 // Generic row degree: the prefix products go through the lr array exactly as
@@ -573,83 +536,23 @@ __global__ __launch_bounds__(256) void k_check_bp_gen(const double* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// BP variable-node phase, regular column degree DV (dec.cpp:667-693):
-//   forward  pr_s = P_s; P_{s+1} = P_s * lr_s; P_0 = LR
-//   P = P_DV; NaN -> 1; dblk = (P <= 1)
-//   backward acc = 1; s = DV-1..0: pr_s *= acc; NaN -> 1; acc *= lr_s
-// then stores d_s = 1 - 2/(1+pr_s) for the next check phase and the ballot of
-// the hard decisions.  Converged lanes keep their state untouched.
-// Tiles t0 .. t0+gridDim.y-1; lr is the group's scratch ([t - t0][E][64]).
-// post (optional) receives P, the posterior ratio of this iteration.
-// grid (ceil(N/4), group tiles), block 256: one wave per (column, tile).
-// ---------------------------------------------------------------------------
-template <int DV, bool NT, bool CSCL, bool CONT>
-__global__ __launch_bounds__(256) void k_var_bp(const double* __restrict__ lr, double* __restrict__ dmsg,
-                                                double* __restrict__ prior, uint64_t* __restrict__ hard,
-                                                const uint64_t* __restrict__ active, const int32_t* __restrict__ col_edge,
-                                                double* __restrict__ post, int32_t N, int64_t E, int64_t t0, Refill rf)
-{
-    const int lane = lane_id();
-    const int32_t j = xcd_block(blockIdx.x, gridDim.x) * 4 + wave_id();
-    const int64_t t = t0 + blockIdx.y;
-    if (j >= N) return;
-    const uint64_t act = active[t];
-    const uint64_t frm = CONT ? rf.fresh[t] : 0ull;
-    const uint64_t touched = act | frm;
-    if (touched == 0) return;
-    const bool live = (act >> lane) & 1ull;
-    int32_t eid[DV];
-#pragma unroll
-    for (int s = 0; s < DV; ++s) eid[s] = col_edge[(size_t)j * DV + s];
-    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
-    bool h = false;
-    const bool fr = CONT && ((frm >> lane) & 1ull);
-    double dv[DV];  // the d values this lane stores (update or initial)
-    const size_t pj = ((size_t)t * N + j) * TILE + lane;
-    if (fr) {  // Init_Belief_Propagation for a refilled lane
-        const double x = rf.in[(size_t)rf.lane_b[t * TILE + lane] * N + j];
-        const double LR = rf.in_is_llr ? exp(x) : x;
-        prior[pj] = LR;
-        const double d0 = 1.0 - 2.0 / (1.0 + LR);
-#pragma unroll
-        for (int s = 0; s < DV; ++s) dv[s] = d0;
-        h = (LR < 1.0);
-    } else if (live) {
-        const double LR = prior[pj];
-        double l[DV], pr[DV];
-#pragma unroll
-        for (int s = 0; s < DV; ++s) l[s] = lr[(tl + (CSCL ? (size_t)j * DV + s : (size_t)eid[s])) * TILE + lane];
-        double p = LR;
-#pragma unroll
-        for (int s = 0; s < DV; ++s) { pr[s] = p; p = p * l[s]; }
-        if (__builtin_isnan(p)) p = 1.0;
-        h = (p <= 1.0);
-        if (post) post[pj] = p;
-        double acc = 1.0;
-#pragma unroll
-        for (int s = DV - 1; s >= 0; --s) {
-            double v = pr[s] * acc;
-            if (__builtin_isnan(v)) v = 1.0;
-            acc = acc * l[s];
-            dv[s] = 1.0 - 2.0 / (1.0 + v);
-        }
-    }
-    if (fr || live) {  // one store sequence for both kinds of lane
-#pragma unroll
-        for (int s = 0; s < DV; ++s) st<NT>(dmsg + (tb + eid[s]) * TILE + lane, dv[s]);
-    }
-    const uint64_t m = __ballot(h);
-    if (lane == 0) {
-        const size_t o = (size_t)t * N + j;
-        const uint64_t old = (touched == ~0ull) ? 0ull : hard[o];
-        hard[o] = (old & ~touched) | (m & touched);
-    }
-}
-
-// Variable phase, CPW consecutive columns per wave, BP (MSA = false, the
-// arithmetic of k_var_bp) or min-sum (MSA = true, that of k_var_msa): every
-// c2v load of the wave's columns is issued before the first column's
-// arithmetic -- fewer, longer-lived waves.  Requires N % (4 * CPW) == 0.
+// Variable-node phase, regular column degree DV, CPW consecutive columns per
+// wave (every c2v load of the wave's columns is issued before the first
+// column's arithmetic -- fewer, longer-lived waves).  Requires N % (4 * CPW)
+// == 0 (CPW = 1: any N).  Per column and lane:
+//   BP (MSA = false, dec.cpp:667-693):
+//     forward  pr_s = P_s; P_{s+1} = P_s * lr_s; P_0 = LR
+//     P = P_DV; NaN -> 1; dblk = (P <= 1)
+//     backward acc = 1; s = DV-1..0: pr_s *= acc; NaN -> 1; acc *= lr_s
+//     then stores d_s = 1 - 2/(1+pr_s) for the next check phase
+//   min-sum (MSA = true, Variable_Update_MSA_INF dec.cpp:1597-1619 +
+//   Decision_MSA_INF dec.cpp:1659-1678):
+//     v2c_s = ((LLR + c_0) + c_1) ... skipping c_s, ascending row order
+//     L = LLR + c_0 + ... + c_{DV-1};  dblk = !(L > 0)
+// and the ballot of the hard decisions; post (optional) receives P / L.
+// CONT: refilled lanes (Refill::fresh) get Init_Belief_Propagation
+// (dec.cpp:608-629) / Init_MSA_INF (dec.cpp:1300-1329) through the same
+// stores, and finished lanes (Refill::fin) get their outputs written first.
 // INPLACE: v2c == c2v (resident pool), see Msg.
 // Column block cb (4 waves x CPW columns) of tile t; c2v_t = the tile's c2v messages.
 template <bool MSA, int DV, bool NT, bool CONT, int CPW, bool INPLACE>
@@ -657,7 +560,7 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
                                             double* __restrict__ prior, uint64_t* __restrict__ hard,
                                             const uint64_t* __restrict__ active, const int32_t* __restrict__ col_edge,
                                             double* __restrict__ post, int32_t N, int64_t E, int64_t t, uint32_t cb,
-                                            const Refill& rf, int full_lanes)
+                                            const Refill& rf)
 {
     const int lane = lane_id();
     const int32_t j0 = ((int32_t)cb * 4 + wave_id()) * CPW;
@@ -693,9 +596,7 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
     if (live) {
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
-            // bit 1 of full_lanes: nontemporal prior loads (keep the c2v group resident)
-            pv[c] = (full_lanes & 2) ? ld<true>(prior + ((size_t)t * N + j0 + c) * TILE + lane)
-                                     : prior[((size_t)t * N + j0 + c) * TILE + lane];
+            pv[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
 #pragma unroll
             for (int s = 0; s < DV; ++s) l[c][s] = c2v_t[(size_t)eid[c][s] * TILE + lane];
         }
@@ -773,14 +674,12 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
                 }
             }
         }
-        // refills: the whole wave stores the prior line (live lanes their own
-        // value) instead of a partial-line write by the refilled lanes alone
-        if (CONT && frm != 0ull && ((full_lanes & 4) || fr)) prior[pj] = np;
+        if (CONT && fr) prior[pj] = np;
         // whole-line stores (others write 0, never read) -- not in a tile that
         // only hands out finished codewords (no live or refilled lane), nor
         // for refills whose first check reads the prior (Refill::prior_only)
         const bool skip_init = CONT && rf.prior_only && !live;
-        if (!skip_init && (((full_lanes & 1) && line_occupied(touched, lane)) || fr || live)) {
+        if (!skip_init && (line_occupied(touched, lane) || fr || live)) {
 #pragma unroll
             for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
         }
@@ -798,46 +697,11 @@ __global__ __launch_bounds__(256) void k_var_m(typename Msg<INPLACE>::in c2v, ty
                                                double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                const uint64_t* __restrict__ active,
                                                const int32_t* __restrict__ col_edge, double* __restrict__ post,
-                                               int32_t N, int64_t E, int64_t t0, Refill rf, int full_lanes)
+                                               int32_t N, int64_t E, int64_t t0, Refill rf)
 {
     var_m_block<MSA, DV, NT, CONT, CPW, INPLACE>(c2v + (size_t)blockIdx.y * E * TILE, v2c, prior, hard, active,
                                                  col_edge, post, N, E, t0 + blockIdx.y,
-                                                 xcd_block(blockIdx.x, gridDim.x), rf, full_lanes);
-}
-
-// Resident pool, ping-pong schedule (engine `pingpong`, BP): ONE launch runs
-// the check phase of pool tile tc (+ its syndrome and lane bookkeeping, as
-// k_check_bp<SYN>) and the variable phase of tile tv, the tile the previous
-// launch checked (+ its finished lanes' outputs and refills, as k_var_m).
-// Blocks of the two kinds are interleaved in dispatch order (nchk check
-// blocks spread evenly over the nchk + nvar blocks of the grid, after the
-// XCD-affine renumbering), so the chip runs both access shapes at once -- the
-// contiguous 72-edge rows beside the scattered 8-edge columns -- instead of
-// whole-pool launches of one shape.  Each tile's phases still alternate check,
-// variable, check, ... in launch order (tv was checked by the previous launch,
-// tc's last variable phase ran P - 1 launches ago, P = pool tiles >= 2), so
-// every codeword's arithmetic is that of k_check_bp / k_var_m.  In place:
-// msg holds the pool's messages (d between the phases, lr inside a step).
-// tv < 0 (the first launch of a decode): nvar == 0.
-template <int DC, int DV, int CPW>
-__global__ __launch_bounds__(256, 2) void k_pingpong_bp(double* msg, double* __restrict__ prior,
-                                                        uint64_t* __restrict__ hard, const uint64_t* __restrict__ active,
-                                                        const int32_t* __restrict__ col_edge,
-                                                        double* __restrict__ post, int32_t M, int32_t N, int64_t E,
-                                                        int64_t tc, int64_t tv, uint32_t nchk, uint32_t nvar,
-                                                        int full_lanes, ResStep rs, Refill rf)
-{
-    const uint32_t T = nchk + nvar;
-    const uint32_t L = xcd_block(blockIdx.x, T);
-    // check blocks before logical block L: floor(L * nchk / T)
-    const uint32_t c0 = (uint32_t)(((uint64_t)L * nchk) / T);
-    const uint32_t c1 = (uint32_t)(((uint64_t)(L + 1) * nchk) / T);
-    if (c1 > c0)
-        check_bp_block<DC, false, false, true, true>(msg, msg + (size_t)tc * E * TILE, active, nullptr, M, E, tc, c0,
-                                                     nchk, full_lanes, rs);
-    else
-        var_m_block<false, DV, false, true, CPW, true>(msg + (size_t)tv * E * TILE, msg, prior, hard, active,
-                                                       col_edge, post, N, E, tv, L - c0, rf, full_lanes);
+                                                 xcd_block(blockIdx.x, gridDim.x), rf);
 }
 
 // Generic column degree: the partial products go through the v2c array
@@ -898,15 +762,14 @@ __global__ __launch_bounds__(256) void k_var_bp_gen(const double* __restrict__ l
 // (x >= 0 ? +1 : -1) (NaN counts -1).  c2v = (double)sign * mag.
 // dc == 1: mag stays -1 -> 0, sign 1 -> 0.0 (dec.cpp:1427-1430).
 // ---------------------------------------------------------------------------
-template <int DC, bool NT, bool CSCL, bool INPLACE>
-__device__ __forceinline__ void check_msa_row(typename Msg<INPLACE>::in src, typename Msg<INPLACE>::out dst,
-                                              const int32_t* __restrict__ prow, int32_t row)
+template <int DC, bool NT, bool INPLACE>
+__device__ __forceinline__ void check_msa_row(typename Msg<INPLACE>::in src, typename Msg<INPLACE>::out dst)
 {
     double x[DC];
 #pragma unroll
     for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
     if constexpr (DC == 1) {
-        dst[(CSCL ? (size_t)prow[0] : (size_t)row) * TILE] = 0.0;
+        dst[0] = 0.0;
         return;
     }
     double m1 = __builtin_inf(), m2 = __builtin_inf();
@@ -931,31 +794,30 @@ __device__ __forceinline__ void check_msa_row(typename Msg<INPLACE>::in src, typ
         if (__builtin_isnan(af)) mag = af;
         const uint32_t nk = (x[k] >= 0) ? 0u : 1u;
         const int sign = ((neg ^ nk) & 1u) ? -1 : 1;
-        const size_t p = CSCL ? (size_t)prow[k] : (size_t)row * DC + k;
-        dst[p * TILE] = (double)sign * mag;
+        dst[(size_t)k * TILE] = (double)sign * mag;
     }
 }
 
-template <int DC, bool NT, bool CSCL, bool SYN, bool INPLACE>
-__global__ __launch_bounds__(256) void k_check_msa(typename Msg<INPLACE>::in v2c, typename Msg<INPLACE>::out c2v,
-                                                   const uint64_t* __restrict__ active,
-                                                   const int32_t* __restrict__ pos, int32_t M, int64_t E,
-                                                   int64_t t0, int full_lanes, ResStep rs)
+// RES: resident pool, as k_check_bp's (in place, row parity, res_arrive).
+template <int DC, bool NT, bool RES>
+__global__ __launch_bounds__(256) void k_check_msa(typename Msg<RES>::in v2c, typename Msg<RES>::out c2v,
+                                                   const uint64_t* __restrict__ active, int32_t M, int64_t E,
+                                                   int64_t t0, ResStep rs)
 {
     const int lane = lane_id();
     const int32_t row = blockIdx.x * 4 + wave_id();
     const int64_t t = t0 + blockIdx.y;
-    const uint64_t act = SYN ? rs.cs.occupied[t] : active[t];
-    // full_lanes: converged / empty lanes of an active tile run along on their
-    // stale state so every c2v store covers whole lines (their values are never read)
-    const bool run = row < M && ((full_lanes & 1) ? line_occupied(act, lane) : ((act >> lane) & 1ull));
-    if constexpr (!SYN) {
+    const uint64_t act = RES ? rs.cs.occupied[t] : active[t];
+    // whole-line policy: converged / empty lanes of an active tile run along on
+    // their stale state so every c2v store covers whole lines (never read)
+    const bool run = row < M && line_occupied(act, lane);
+    if constexpr (!RES) {
         if (!run) return;
     }
     uint64_t par = 0;
     int32_t ln0 = 0;
     int64_t b0 = 0;
-    if (SYN && act != 0) {
+    if (RES && act != 0) {
         // the lane state for res_arrive's bookkeeping (used by the tile's last
         // block only), loaded up front so it is not on the tail's chain
         if (threadIdx.x < TILE && ((act >> lane) & 1ull)) {
@@ -965,9 +827,9 @@ __global__ __launch_bounds__(256) void k_check_msa(typename Msg<INPLACE>::in v2c
         if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
     }
     if (run)
-        check_msa_row<DC, NT, CSCL, INPLACE>(v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane,
-                                    c2v + (size_t)blockIdx.y * E * TILE + lane, pos + (size_t)row * DC, row);
-    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0, gridDim.x);
+        check_msa_row<DC, NT, RES>(v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane,
+                                   c2v + ((size_t)blockIdx.y * E + (size_t)row * DC) * TILE + lane);
+    if constexpr (RES) res_arrive(t, act, par, rs, ln0, b0, gridDim.x);
 }
 
 __global__ __launch_bounds__(256) void k_check_msa_gen(const double* __restrict__ v2c, double* __restrict__ c2v,
@@ -1011,72 +873,6 @@ __global__ __launch_bounds__(256) void k_check_msa_gen(const double* __restrict_
     }
 }
 
-// ---------------------------------------------------------------------------
-// Min-sum variable-node phase + decision (Variable_Update_MSA_INF
-// dec.cpp:1597-1619, Decision_MSA_INF dec.cpp:1659-1678):
-//   v2c_s = ((LLR + c_0) + c_1) ... skipping c_s, ascending row order
-//   L = LLR + c_0 + ... + c_{DV-1};  dblk = !(L > 0);  post (optional) <- L
-// ---------------------------------------------------------------------------
-template <int DV, bool NT, bool CSCL, bool CONT>
-__global__ __launch_bounds__(256) void k_var_msa(const double* __restrict__ c2v, double* __restrict__ v2c,
-                                                 double* __restrict__ prior, uint64_t* __restrict__ hard,
-                                                 const uint64_t* __restrict__ active, const int32_t* __restrict__ col_edge,
-                                                 double* __restrict__ post, int32_t N, int64_t E, int64_t t0, Refill rf)
-{
-    const int lane = lane_id();
-    const int32_t j = xcd_block(blockIdx.x, gridDim.x) * 4 + wave_id();
-    const int64_t t = t0 + blockIdx.y;
-    if (j >= N) return;
-    const uint64_t act = active[t];
-    const uint64_t frm = CONT ? rf.fresh[t] : 0ull;
-    const uint64_t touched = act | frm;
-    if (touched == 0) return;
-    const bool live = (act >> lane) & 1ull;
-    int32_t eid[DV];
-#pragma unroll
-    for (int s = 0; s < DV; ++s) eid[s] = col_edge[(size_t)j * DV + s];
-    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
-    bool h = false;
-    const bool fr = CONT && ((frm >> lane) & 1ull);
-    double dv[DV];  // the v2c values this lane stores (update or initial)
-    const size_t pj = ((size_t)t * N + j) * TILE + lane;
-    if (fr) {  // Init_MSA_INF for a refilled lane
-        const double x = rf.in[(size_t)rf.lane_b[t * TILE + lane] * N + j];
-        prior[pj] = x;
-#pragma unroll
-        for (int s = 0; s < DV; ++s) dv[s] = x;
-        h = !(x > 0);
-    } else if (live) {
-        const double llr = prior[pj];
-        double c[DV];
-#pragma unroll
-        for (int s = 0; s < DV; ++s) c[s] = c2v[(tl + (CSCL ? (size_t)j * DV + s : (size_t)eid[s])) * TILE + lane];
-#pragma unroll
-        for (int s = 0; s < DV; ++s) {
-            double sum = llr;
-#pragma unroll
-            for (int r = 0; r < DV; ++r)
-                if (r != s) sum = sum + c[r];
-            dv[s] = sum;
-        }
-        double L = llr;
-#pragma unroll
-        for (int s = 0; s < DV; ++s) L = L + c[s];
-        h = !(L > 0);
-        if (post) post[pj] = L;
-    }
-    if (fr || live) {  // one store sequence for both kinds of lane
-#pragma unroll
-        for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[s]) * TILE + lane, dv[s]);
-    }
-    const uint64_t m = __ballot(h);
-    if (lane == 0) {
-        const size_t o = (size_t)t * N + j;
-        const uint64_t old = (touched == ~0ull) ? 0ull : hard[o];
-        hard[o] = (old & ~touched) | (m & touched);
-    }
-}
-
 __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ c2v, double* __restrict__ v2c,
                                                      const double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                      const uint64_t* __restrict__ active, const int32_t* __restrict__ col_ptr,
@@ -1117,33 +913,50 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// Compressed min-sum check->variable messages ("MSA-C", regular graphs).
-// A row's 72 outgoing messages take only four magnitudes -- min1, min2 and,
-// in the NaN cases derived above k_check_msa, |x_0| or |x_1| -- and a sign, so
-// the check phase writes per (row, lane) a record of those magnitudes and per
-// edge one code byte instead of 72 fp64 messages:
-//   rec   [group tile][M][4][64] fp64   planes m1, m2, n0 = |x_0|, n1 = |x_1|
-//                                       (n0 / n1 written only when NaN)
-//   codes [group tile][E][64] u8        bit 0: sign -1; bits 1-2: source plane
-// The variable phase rebuilds c2v = (double)sign * plane[source] -- the value
-// k_check_msa stores, by the same expression -- so every downstream sum is
-// unchanged.  Per edge and codeword the c2v stream shrinks from 16 B (write +
-// read) to 2 B plus the record (1 KB per row and wave, read 72 times while
-// resident in the XCD's L2; see k_var_msa_c for the XCD-affine tile order).
+// Compressed min-sum check->variable messages ("MSA-C", (DC, DV)-regular
+// graphs with E < 2^18).  A row's DC outgoing messages take only four
+// magnitudes -- min1, min2 and, in the NaN cases derived above k_check_msa,
+// |x_0| or |x_1| -- and a sign, so the check phase writes per (row, lane):
+//   rec  [group tile][M][64] {min1, min2}: 16 B per lane, one contiguous
+//        1-KB store per wave (and one 16-B load per lane and edge in the
+//        variable phase, independent of the meta word)
+//   meta [group tile][M][64] u32: bit 31 the row's sign parity, bit 30 NaN at
+//        x_1, bit 29 NaN at x_0, bits 0-17 the edge id of min1 (row * DC +
+//        i1; MSA_META_NONE: no minimum, every |x| inf or NaN)
+//   nanp [group tile][M][2][64] fp64 |x_0|, |x_1| -- written only when NaN
+// and nothing per edge.  The variable phase rebuilds each c2v from the meta
+// word, its own edge id and the sign bit of the v2c it stored itself (sgn,
+// !(x >= 0) of exactly that value -- the check's sign rule):
+//   sign = parity ^ own; mag = (edge == min1 edge) ? min2 : min1, or the NaN
+//   plane (|x_1| for the row's first edge, |x_0| for the others)
+//   c2v = mag with its sign bit flipped when sign is negative
+// which is k_check_msa's (double)sign * mag for every non-NaN mag (+-0, +-inf
+// included); a NaN's sign is never observed downstream (comparisons, fabs and
+// sums only), so every sum and decision is unchanged.  Per edge and codeword
+// the c2v stream shrinks from 16 B (fp64 write + read) to the records, which
+// the row's DC columns re-read from the XCD's L2 (see k_var_msa_c).
 // ---------------------------------------------------------------------------
-constexpr int MSA_REC_PLANES = 4;
 constexpr uint32_t MSA_META_NONE = 0x3ffffu;  // meta: no min1 (edge ids must stay below it)
 
-template <int DC, bool NT>
-__device__ __forceinline__ void check_msa_c_row(const double* __restrict__ v2c, uint8_t* __restrict__ codes,
-                                                double* __restrict__ rec, uint32_t* __restrict__ meta, int32_t M,
-                                                int64_t E, int64_t t, int32_t row)
+// grid (ceil(M/4), group tiles), block 256: one wave per (row, tile); the
+// v2c group is streamed once, nontemporal.
+template <int DC>
+__global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, double2* __restrict__ rec,
+                                                     uint32_t* __restrict__ meta, double* __restrict__ nanp,
+                                                     const uint64_t* __restrict__ active, int32_t M, int64_t E,
+                                                     int64_t t0)
 {
+    static_assert(DC >= 2 && DC <= 96, "row degree");
     const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = t0 + blockIdx.y;
+    const uint64_t act = active[t];
+    // whole-line policy (as k_check_msa)
+    if (!(row < M && line_occupied(act, lane))) return;
     const double* __restrict__ src = v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
     double x[DC];
 #pragma unroll
-    for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
+    for (int k = 0; k < DC; ++k) x[k] = ld<true>(src + (size_t)k * TILE);
     // one pass: min1 with its FIRST index, min2 = minimum over the other
     // indices (a tie with min1 gives min2 == min1), NaN never compares less
     double m1 = __builtin_inf(), m2 = __builtin_inf();
@@ -1166,83 +979,36 @@ __device__ __forceinline__ void check_msa_c_row(const double* __restrict__ v2c, 
     neg &= 1u;
     const double a0 = __builtin_fabs(x[0]), a1 = __builtin_fabs(x[1]);
     const bool nan0 = __builtin_isnan(a0), nan1 = __builtin_isnan(a1);
-    double* __restrict__ r = rec + ((size_t)blockIdx.y * M + row) * (MSA_REC_PLANES * TILE) + lane;
-    r[0] = m1;
-    r[TILE] = m2;
-    if (nan0) r[2 * TILE] = a0;
-    if (nan1) r[3 * TILE] = a1;
-    if (meta) {
-        // MSA-C without codes: 32 bits per (row, lane) -- bit 31 the row's sign
-        // parity, bit 30 NaN at x_1, bit 29 NaN at x_0, bits 0-17 the edge id
-        // of min1 (row * DC + i1; MSA_META_NONE: no minimum, every |x| inf or
-        // NaN).  The variable phase rebuilds each edge's code from it, its
-        // own edge id and the sign bit it stored itself with the v2c (the same
-        // !(x >= 0) as negb).
-        meta[((size_t)blockIdx.y * M + row) * TILE + lane] =
-            (neg << 31) | ((nan1 ? 1u : 0u) << 30) | ((nan0 ? 1u : 0u) << 29) |
-            (i1 < 0 ? MSA_META_NONE : (uint32_t)(row * DC + i1));
-        return;
-    }
-    uint8_t* __restrict__ c = codes + ((size_t)blockIdx.y * E + (size_t)row * DC) * TILE + lane;
-#pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        const uint32_t nk = (negb[k / 32] >> (k % 32)) & 1u;
-        const bool nanf = (k == 0) ? nan1 : nan0;
-        const uint32_t srcp = nanf ? (k == 0 ? 3u : 2u) : (k == i1 ? 1u : 0u);
-        c[(size_t)k * TILE] = (uint8_t)((neg ^ nk) | (srcp << 1));
-    }
+    const size_t ri = ((size_t)blockIdx.y * M + row) * TILE + lane;
+    rec[ri] = make_double2(m1, m2);
+    meta[ri] = (neg << 31) | ((nan1 ? 1u : 0u) << 30) | ((nan0 ? 1u : 0u) << 29) |
+               (i1 < 0 ? MSA_META_NONE : (uint32_t)(row * DC + i1));
+    double* __restrict__ np = nanp + ((size_t)blockIdx.y * M + row) * (2 * TILE) + lane;
+    if (nan0) np[0] = a0;
+    if (nan1) np[TILE] = a1;
 }
 
-// SYN (resident pool, ResStep): as k_check_bp's -- the lanes run are the
-// tile's occupied ones, each wave also takes its row's parity over the
-// previous variable phase's ballots, every block ends in res_arrive.
-template <int DC, bool NT, bool SYN>
-__global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, uint8_t* __restrict__ codes,
-                                                     double* __restrict__ rec, uint32_t* __restrict__ meta,
-                                                     const uint64_t* __restrict__ active,
-                                                     int32_t M, int64_t E, int64_t t0, int full_lanes, ResStep rs)
+__device__ __forceinline__ double flip_sign(double v, uint32_t neg)
 {
-    static_assert(DC >= 2 && DC <= 96, "row degree");
-    const int lane = lane_id();
-    const int32_t row = blockIdx.x * 4 + wave_id();
-    const int64_t t = t0 + blockIdx.y;
-    const uint64_t act = SYN ? rs.cs.occupied[t] : active[t];
-    const bool run = row < M && ((full_lanes & 1) ? line_occupied(act, lane) : ((act >> lane) & 1ull));
-    if constexpr (!SYN) {
-        if (!run) return;
-    }
-    uint64_t par = 0;
-    int32_t ln0 = 0;
-    int64_t b0 = 0;
-    if (SYN && act != 0) {
-        if (threadIdx.x < TILE && ((act >> lane) & 1ull)) {
-            ln0 = rs.cs.lane_n[t * TILE + lane];
-            b0 = rs.cs.lane_b[t * TILE + lane];
-        }
-        if (row < M) par = row_parity<DC>(rs.hard + (size_t)t * rs.N, rs.col_idx + (size_t)row * DC);
-    }
-    if (run) check_msa_c_row<DC, NT>(v2c, codes, rec, meta, M, E, t, row);
-    if constexpr (SYN) res_arrive(t, act, par, rs, ln0, b0, gridDim.x);
+    return __longlong_as_double(__double_as_longlong(v) ^ ((long long)(neg & 1u) << 63));
 }
 
-// Min-sum variable phase on compressed messages (arithmetic of k_var_m<MSA>).
+// Min-sum variable phase on compressed messages (the arithmetic of k_var_m<MSA>).
 // 1-D grid of gt * (N / (4 CPW)) blocks; block L works on group tile L % gt.
 // Workgroups are dispatched to the 8 XCDs round-robin, so when gt divides 8
-// every XCD only ever touches the records of one tile (2 MB), which stay in
-// its 4 MB L2 while they are re-read by the tile's 72 columns per row.
-// META (meta != nullptr at the check): codes rebuilt from the row's 32-bit meta word
-// (parity, NaN flags, edge id of min1), the edge's own id
-// and the sign byte this kernel stored with the column's v2c (sgn, one bit per
-// edge: the check's sign bit is !(x >= 0) of exactly that value); no code
-// bytes are written or read.
-template <int DV, bool NT, bool CONT, int CPW, bool SEL2 = false, bool META = false>
-__global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ codes, const double* __restrict__ rec,
-                                                   double* __restrict__ v2c, double* __restrict__ prior,
-                                                   uint64_t* __restrict__ hard, const uint64_t* __restrict__ active,
+// every XCD only ever touches the records of one tile (2.5 MB for the DNA
+// code), which stay in its 4 MB L2 while the tile's DC columns per row re-read
+// them.  Every record and meta load of the wave's CPW columns is issued before
+// the first use (no load depends on another), and the v2c stores are
+// nontemporal (the group's v2c is read back once, by the next check phase).
+template <int DC, int DV, bool CONT, int CPW>
+__global__ __launch_bounds__(256) void k_var_msa_c(const double2* __restrict__ rec, const uint32_t* __restrict__ meta,
+                                                   const double* __restrict__ nanp, double* __restrict__ v2c,
+                                                   double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                                   uint8_t* __restrict__ sgn, const uint64_t* __restrict__ active,
                                                    const int32_t* __restrict__ col_edge,
                                                    const int32_t* __restrict__ col_row, double* __restrict__ post,
-                                                   int32_t N, int32_t M, int64_t E, int64_t t0, uint32_t gt, Refill rf,
-                                                   int full_lanes, const uint32_t* __restrict__ meta, uint8_t* sgn)
+                                                   int32_t N, int32_t M, int64_t E, int64_t t0, uint32_t gt, Refill rf)
 {
     const int lane = lane_id();
     const uint32_t ty = blockIdx.x % gt;
@@ -1252,8 +1018,8 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
     const uint64_t act = active[t];
     const uint64_t frm = CONT ? rf.fresh[t] : 0ull;
     const uint64_t touched = act | frm;
-    // resident pool: lanes whose codeword finished at this step's syndrome
-    // (outputs written here, before a refill overwrites the lane; as k_var_m)
+    // lanes whose codeword finished at this step's syndrome (outputs written
+    // here, before a refill overwrites the lane; as k_var_m)
     const uint64_t fm = (CONT && rf.fin) ? rf.fin[t] : 0ull;
     if (touched == 0 && fm == 0) return;
     const bool live = (act >> lane) & 1ull;
@@ -1274,8 +1040,9 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
             eid[c][s] = col_edge[(size_t)(j0 + c) * DV + s];
             rid[c][s] = col_row[(size_t)(j0 + c) * DV + s];
         }
-    const uint8_t* __restrict__ cg = codes + (size_t)ty * E * TILE + lane;
-    const double* __restrict__ rg = rec + (size_t)ty * M * (MSA_REC_PLANES * TILE) + lane;
+    // wave-uniform bases: per-edge addresses are a scalar base + the lane offset
+    const double2* __restrict__ rg = rec + (size_t)ty * M * TILE;
+    const uint32_t* __restrict__ mg = meta + (size_t)ty * M * TILE;
     double l[CPW][DV], pv[CPW], xin[CPW];
     if (fr) {
         const double* __restrict__ in_row = rf.in + (size_t)rf.lane_b[t * TILE + lane] * N;
@@ -1283,101 +1050,42 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
         for (int c = 0; c < CPW; ++c) xin[c] = in_row[j0 + c];
     }
     if (live) {
-        // codes: one byte per edge (cd), or with META one 4-bit code per edge
-        // packed 8 to a register (cpk; fewer VGPRs live across the gathers)
-        uint32_t cd[META ? 1 : CPW][DV], cpk[CPW];
-        auto code = [&](int c, int s) -> uint32_t {
-            if constexpr (META) return (cpk[c] >> (4 * s)) & 15u;
-            else return cd[c][s];
-        };
+        uint32_t sb[CPW], mw[CPW][DV];
+        double2 rr[CPW][DV];
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             pv[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
-            if constexpr (!META) {
+            sb[c] = sgn[((size_t)t * N + j0 + c) * TILE + lane];
 #pragma unroll
-                for (int s = 0; s < DV; ++s) cd[META ? 0 : c][s] = cg[(size_t)eid[c][s] * TILE];
+            for (int s = 0; s < DV; ++s) {
+                mw[c][s] = (mg + (size_t)rid[c][s] * TILE)[lane];
+                rr[c][s] = (rg + (size_t)rid[c][s] * TILE)[lane];
             }
         }
-        if constexpr (META) {
-            const uint32_t* __restrict__ mg = meta + (size_t)ty * M * TILE + lane;
-            uint32_t sb[CPW], anynan = 0;
-#pragma unroll
-            for (int c = 0; c < CPW; ++c) {
-                sb[c] = sgn[((size_t)t * N + j0 + c) * TILE + lane];
-#pragma unroll
-                for (int s = 0; s < DV; ++s) {
-                    // code of the edge (as check_msa_c_row's): sign = parity ^
-                    // own sign, plane 1 iff it is the row's min1 edge
-                    const uint32_t m = mg[(size_t)rid[c][s] * TILE];
-                    anynan |= m;
-                    const uint32_t q = ((m >> 31) ^ ((sb[c] >> s) & 1u)) |
-                                       ((m & MSA_META_NONE) == (uint32_t)eid[c][s] ? 2u : 0u);
-                    cpk[c] = (s == 0 ? 0u : cpk[c]) | (q << (4 * s));
-                }
-            }
-            if (__builtin_expect(__ballot((anynan >> 29) & 3u) != 0ull, 0)) {
-                // a row with NaN at x_0 / x_1: planes 3 (k = 0) / 2 (k > 0)
-                constexpr int32_t DCR = 72;  // row degree (MSA-C runs on the (8,72)-regular graph only)
-#pragma unroll
-                for (int c = 0; c < CPW; ++c)
-#pragma unroll
-                    for (int s = 0; s < DV; ++s) {
-                        const uint32_t m = mg[(size_t)rid[c][s] * TILE];
-                        const bool first = eid[c][s] % DCR == 0;  // edges are numbered row-major
-                        if ((m >> (first ? 30 : 29)) & 1u)
-                            cpk[c] = (cpk[c] & ~(6u << (4 * s))) | ((first ? 3u : 2u) << (4 * s + 1));
-                    }
-            }
-        }
-        if constexpr (SEL2) {
-            // min1 and min2 planes both loaded (whole 512-B segments, no
-            // dependence on the code); the NaN planes only when a lane needs one
-            double ma[CPW][DV], mb[CPW][DV];
-            uint32_t nanm = 0;
-#pragma unroll
-            for (int c = 0; c < CPW; ++c)
-#pragma unroll
-                for (int s = 0; s < DV; ++s) {
-                    const double* rr = rg + (size_t)rid[c][s] * (MSA_REC_PLANES * TILE);
-                    ma[c][s] = rr[0];
-                    mb[c][s] = rr[TILE];
-                }
-#pragma unroll
-            for (int c = 0; c < CPW; ++c)
-#pragma unroll
-                for (int s = 0; s < DV; ++s) {
-                    const uint32_t sp = (code(c, s) >> 1) & 3u;
-                    l[c][s] = (sp & 1u) ? mb[c][s] : ma[c][s];
-                    nanm |= sp >> 1;
-                }
-            if (__builtin_expect(nanm != 0, 0)) {
-#pragma unroll
-                for (int c = 0; c < CPW; ++c)
-#pragma unroll
-                    for (int s = 0; s < DV; ++s) {
-                        const uint32_t sp = (code(c, s) >> 1) & 3u;
-                        const size_t o = ((size_t)rid[c][s] * MSA_REC_PLANES + (sp | 2u)) * TILE;
-                        const double nv = rg[o];  // harmless extra read for lanes that do not use it
-                        if (sp >= 2) l[c][s] = nv;
-                    }
-            }
-        } else {
-            // one record load per edge, from the plane the code names
-#pragma unroll
-            for (int c = 0; c < CPW; ++c)
-#pragma unroll
-                for (int s = 0; s < DV; ++s) {
-                    const uint32_t sp = (code(c, s) >> 1) & 3u;
-                    l[c][s] = rg[((size_t)rid[c][s] * MSA_REC_PLANES + sp) * TILE];
-                }
-        }
+        uint32_t anynan = 0;
 #pragma unroll
         for (int c = 0; c < CPW; ++c)
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
-                const int sign = (code(c, s) & 1u) ? -1 : 1;
-                l[c][s] = (double)sign * l[c][s];
+                const uint32_t m = mw[c][s];
+                anynan |= m;
+                const double mag = ((m & MSA_META_NONE) == (uint32_t)eid[c][s]) ? rr[c][s].y : rr[c][s].x;
+                l[c][s] = flip_sign(mag, (m >> 31) ^ (sb[c] >> s));
             }
+        if (__builtin_expect(__ballot((anynan >> 29) & 3u) != 0ull, 0)) {
+            // a row with NaN at x_0 / x_1: |x_1| for the row's first edge, |x_0| for the others
+#pragma unroll
+            for (int c = 0; c < CPW; ++c)
+#pragma unroll
+                for (int s = 0; s < DV; ++s) {
+                    const uint32_t m = mw[c][s];
+                    const bool first = eid[c][s] % DC == 0;  // edges are numbered row-major
+                    if ((m >> (first ? 30 : 29)) & 1u) {
+                        const double nv = nanp[((size_t)ty * M + rid[c][s]) * (2 * TILE) + (first ? TILE : 0) + lane];
+                        l[c][s] = flip_sign(nv, (m >> 31) ^ (sb[c] >> s));
+                    }
+                }
+        }
     }
     if (CONT && fl) {  // finished codeword: hard bits of its exit (ballots before this step's update)
         uint64_t hw[CPW];
@@ -1397,39 +1105,35 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const uint8_t* __restrict__ c
         double dv[DV];
 #pragma unroll
         for (int s = 0; s < DV; ++s) dv[s] = 0.0;
-        double np = 0.0;
-        if (live) np = pv[c];
         if (fr) {  // Init_MSA_INF for a refilled lane
             const double x = xin[c];
-            np = x;
 #pragma unroll
             for (int s = 0; s < DV; ++s) dv[s] = x;
             h = !(x > 0);
-        } else if (live) {  // v2c_s = LLR + c_0 + ... (skipping c_s); L = LLR + all
+        } else if (live) {
+            // v2c_s = LLR + c_0 + ... (skipping c_s), L = LLR + all, in the
+            // reference's left-to-right order: v2c_s continues the shared
+            // prefix P_s = LLR + c_0 + ... + c_{s-1} with c_{s+1} .. c_{DV-1}
+            double P = pv[c];
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
-                double sum = pv[c];
+                double sum = P;
 #pragma unroll
-                for (int q = 0; q < DV; ++q)
-                    if (q != s) sum = sum + l[c][q];
+                for (int q = s + 1; q < DV; ++q) sum = sum + l[c][q];
                 dv[s] = sum;
+                P = P + l[c][s];
             }
-            double L = pv[c];
-#pragma unroll
-            for (int s = 0; s < DV; ++s) L = L + l[c][s];
-            h = !(L > 0);
-            if (post) post[pj] = L;
+            h = !(P > 0);
+            if (post) post[pj] = P;
         }
-        if (CONT && frm != 0ull && ((full_lanes & 4) || fr)) prior[pj] = np;
-        if (((full_lanes & 1) && line_occupied(touched, lane)) || fr || live) {  // as k_var_m
+        if (CONT && fr) prior[pj] = xin[c];
+        if (line_occupied(touched, lane) || fr || live) {  // whole-line stores, as k_var_m
 #pragma unroll
-            for (int s = 0; s < DV; ++s) st<NT>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
-            if constexpr (META) {
-                uint32_t sbn = 0;
+            for (int s = 0; s < DV; ++s) st<true>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
+            uint32_t sbn = 0;
 #pragma unroll
-                for (int s = 0; s < DV; ++s) sbn |= (dv[s] >= 0 ? 0u : 1u) << s;
-                sgn[pj] = (uint8_t)sbn;
-            }
+            for (int s = 0; s < DV; ++s) sbn |= (dv[s] >= 0 ? 0u : 1u) << s;
+            sgn[pj] = (uint8_t)sbn;
         }
         const uint64_t m = __ballot(h);
         if (lane == 0 && touched) {
@@ -1500,51 +1204,6 @@ __global__ __launch_bounds__(256) void k_cont_reset(uint64_t* __restrict__ activ
         if (done) done[i] = 0;
     }
     if (blockIdx.x == 0 && (int32_t)threadIdx.x < nctr) ctr[threadIdx.x] = 0;
-}
-
-// one block per tile
-template <int DC>
-__global__ __launch_bounds__(1024) void k_syndrome_cont(const uint64_t* __restrict__ hard,
-                                                        const int32_t* __restrict__ row_ptr,
-                                                        const int32_t* __restrict__ col_idx,
-                                                        const int32_t* __restrict__ col_idx_T, int32_t M, int32_t N,
-                                                        int32_t max_iter, ContState cs, ContOut co)
-{
-    __shared__ uint64_t red[16];
-    __shared__ int64_t s_b[TILE];
-    __shared__ int32_t s_n[TILE];
-    __shared__ uint64_t s_fin;
-    const int64_t t = blockIdx.x;
-    const uint64_t occ = cs.occupied[t];
-    const int lane = lane_id(), w = wave_id();
-    const uint64_t* h = hard + (size_t)t * N;
-    uint64_t u = 0;
-    if (occ) {
-        for (int32_t i = threadIdx.x; i < M; i += blockDim.x) {
-            uint64_t p = 0;
-            if (DC > 0) {
-#pragma unroll 24
-                for (int k = 0; k < DC; ++k) p ^= h[col_idx_T[(size_t)k * M + i]];
-            } else {
-                for (int32_t e = row_ptr[i]; e < row_ptr[i + 1]; ++e) p ^= h[col_idx[e]];
-            }
-            u |= p;
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) u |= shfl_xor_u64(u, off);
-        if (lane == 0) red[w] = u;
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        uint64_t U = 0;
-        if (occ)
-            for (int q = 0; q < (int)(blockDim.x >> 6); ++q) U |= red[q];
-        const size_t li = (size_t)t * TILE + lane;
-        const bool o = (occ >> lane) & 1ull;
-        cont_lanes(t, occ, U, max_iter, cs, co, s_b, s_n, &s_fin, o ? cs.lane_n[li] : 0, o ? cs.lane_b[li] : -1, true);
-    }
-    __syncthreads();
-    if (s_fin) cont_outputs(t, s_fin, h, N, co, s_b, s_n);
 }
 
 // Continuous-batching syndrome spread over gridDim.x blocks per tile (the

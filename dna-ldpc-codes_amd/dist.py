@@ -68,6 +68,14 @@ class Group:
     def sum(self, x: float) -> float:
         return self._reduce(x, "SUM")
 
+    def gather(self, obj) -> list:
+        """Every rank's `obj` (a small picklable value), in rank order."""
+        if self._pg is None:
+            return [obj]
+        out = [None] * self.world
+        self._pg.all_gather_object(out, obj)
+        return out
+
     def barrier(self):
         if self._pg is not None:
             self._pg.barrier()

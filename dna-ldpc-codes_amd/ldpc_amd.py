@@ -17,6 +17,7 @@ is visible, every decode raises.
 from __future__ import annotations
 
 import ctypes as C
+import enum
 import math
 import os
 import threading
@@ -28,20 +29,36 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libldpc_amd.so")
 
+ABI_VERSION = 2
 LDPC_OK, LDPC_ERR_ARG, LDPC_ERR_IO, LDPC_ERR_FORMAT, LDPC_ERR_DEVICE, LDPC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
-ALGO_BP, ALGO_MSA, ALGO_QMSA, ALGO_GALLAGER_A, ALGO_GALLAGER_B1, ALGO_GALLAGER_B2 = 0, 1, 2, 3, 4, 5
+
+
+class Algo(enum.IntEnum):
+    """The ABI's LDPC_ALGO_* codes.  A plain int passed as `algo` is the
+    reference's decoder_type instead (DECODER_TYPES below); these members are
+    recognised as ABI codes by their type."""
+    BP = 0
+    MSA = 1
+    QMSA = 2
+    GALLAGER_A = 3
+    GALLAGER_B1 = 4
+    GALLAGER_B2 = 5
+
+
+ALGO_BP, ALGO_MSA, ALGO_QMSA = Algo.BP, Algo.MSA, Algo.QMSA
+ALGO_GALLAGER_A, ALGO_GALLAGER_B1, ALGO_GALLAGER_B2 = Algo.GALLAGER_A, Algo.GALLAGER_B1, Algo.GALLAGER_B2
 POST_LLR, POST_RATIO = 0, 1
 IN_LLR, IN_LR = 0, 1
 H2D, D2H, D2D = 0, 1, 2
 
-# Algorithm selection.  Names select the ABI's LDPC_ALGO_* decoders; an int
-# is the reference's decoder_type (enum DECODER_TYPE, DNA_main.cpp:41-53),
-# mapped as LDPC_Decode (DNA_main.cpp:1565-1594) dispatches it and as bin/ldpc
-# does: 0 BP, 1/2/3 Gallager A/B1/B2, 20/21/22 the float min-sum
-# Run_MSA_Decoder_INF (the DNA build never sets g_precision, so the quantized
-# Run_MSA_Decoder is unreachable from a decoder_type; use the name 'qmsa').
-# The ABI codes themselves are reachable only through the names, so a
-# reference caller's decoder_type never silently picks another decoder.
+# Algorithm selection.  Names and Algo members select the ABI's LDPC_ALGO_*
+# decoders; a plain int is the reference's decoder_type (enum DECODER_TYPE,
+# DNA_main.cpp:41-53), mapped as LDPC_Decode (DNA_main.cpp:1565-1594)
+# dispatches it and as bin/ldpc does: 0 BP, 1/2/3 Gallager A/B1/B2, 20/21/22
+# the float min-sum Run_MSA_Decoder_INF (the DNA build never sets g_precision,
+# so the quantized Run_MSA_Decoder is unreachable from a decoder_type; use
+# 'qmsa' or Algo.QMSA).  A reference caller's decoder_type never silently picks
+# another decoder, and neither does this module's own ALGO_* constant.
 _NAMES = {"bp": ALGO_BP, "msa": ALGO_MSA, "min-sum": ALGO_MSA, "qmsa": ALGO_QMSA,
           "gallager_a": ALGO_GALLAGER_A, "gallager_b1": ALGO_GALLAGER_B1, "gallager_b2": ALGO_GALLAGER_B2}
 DECODER_TYPES = {0: ALGO_BP, 1: ALGO_GALLAGER_A, 2: ALGO_GALLAGER_B1, 3: ALGO_GALLAGER_B2,
@@ -57,11 +74,49 @@ class LdpcError(RuntimeError):
         self.code = code
 
 
+# ldpc_schedule flag bits (include/ldpc_amd.h LDPC_SCHED_*) by keyword
+SCHED_FLAGS = {"nontemporal": 1 << 0, "continuous": 1 << 3, "msa_compressed": 1 << 4, "resident": 1 << 5,
+               "split_syndrome": 1 << 6, "first_from_prior": 1 << 12, "lr_table": 1 << 13,
+               "debug_no_drain": 1 << 14}
+SCHED_FIELDS = ("group_tiles", "var_cpw", "pool_tiles", "poll_every", "syn_blocks")
+
+
+class Schedule(C.Structure):
+    """ldpc_schedule: how a decode is laid out over launches (never what it
+    computes).  Schedule.make(resident=False, group_tiles=2, ...) -- unset
+    keywords keep the library's defaults."""
+    _fields_ = [("flags_set", C.c_int32), ("flags", C.c_int32), ("group_tiles", C.c_int32), ("var_cpw", C.c_int32),
+                ("pool_tiles", C.c_int32), ("poll_every", C.c_int32), ("syn_blocks", C.c_int32),
+                ("reserved", C.c_int32)]
+
+    @classmethod
+    def make(cls, **kw) -> "Schedule":
+        s = cls()
+        for k, v in kw.items():
+            if v is None:
+                continue
+            if k in SCHED_FLAGS:
+                s.flags_set |= SCHED_FLAGS[k]
+                if v:
+                    s.flags |= SCHED_FLAGS[k]
+            elif k in SCHED_FIELDS:
+                setattr(s, k, int(v))
+            else:
+                raise TypeError(f"unknown schedule keyword {k!r} (flags: {sorted(SCHED_FLAGS)}, fields: {SCHED_FIELDS})")
+        return s
+
+
+def _schedule(schedule) -> Optional[Schedule]:
+    if schedule is None or isinstance(schedule, Schedule):
+        return schedule
+    return Schedule.make(**dict(schedule))
+
+
 class Opts(C.Structure):
     _fields_ = [("n_devices", C.c_int32), ("devices", C.POINTER(C.c_int32)), ("chunk", C.c_int64),
                 ("exp_on_host", C.c_int32), ("post_kind", C.c_int32), ("host_threads", C.c_int32),
                 ("msa_precision", C.c_int32), ("msa_offset", C.c_int32), ("reserved0", C.c_int32),
-                ("msa_step", C.c_double), ("tie_seed", C.c_uint64)]
+                ("msa_step", C.c_double), ("tie_seed", C.c_uint64), ("schedule", C.POINTER(Schedule))]
 
 
 class KernelStats(C.Structure):
@@ -78,7 +133,7 @@ EXPORTS = [
     "ldpc_graph_load_alist", "ldpc_graph_rs_ldpc", "ldpc_graph_save_pchk", "ldpc_graph_save_alist",
     "ldpc_graph_free", "ldpc_graph_info", "ldpc_graph_blocks", "ldpc_graph_edges", "ldpc_graph_syndrome", "ldpc_decode",
     "ldpc_engine_create", "ldpc_engine_create_ex", "ldpc_engine_info", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
-    "ldpc_engine_gen_bsc", "ldpc_engine_set_params", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_engine_wall", "ldpc_dev_malloc", "ldpc_dev_free",
+    "ldpc_engine_gen_bsc", "ldpc_engine_set_params", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
     "ldpc_dev_memcpy", "ldpc_dna_llr", "ldpc_dna_edit_distance", "ldpc_write_soft_files", "ldpc_py_float_repr",
 ]
 
@@ -93,6 +148,9 @@ def lib():
             raise ImportError(f"{LIB_PATH} is missing: build it with `make -C dna-ldpc-codes_amd` "
                               "(there is no CPU fallback)")
         L = C.CDLL(LIB_PATH)
+        if L.ldpc_abi_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH}: ABI version {L.ldpc_abi_version()}, this shim needs {ABI_VERSION} "
+                              "(rebuild with `make -C dna-ldpc-codes_amd`)")
         vp, i32, i64, dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_double
         pint = C.POINTER(C.c_int)
         L.ldpc_abi_version.restype = C.c_int
@@ -117,7 +175,7 @@ def lib():
         L.ldpc_decode.argtypes = [vp, vp, i64, i32, i32, vp, vp, vp, vp, C.POINTER(Opts)]
         L.ldpc_engine_create.argtypes = [vp, i32, i32, i64, pint]
         L.ldpc_engine_create.restype = vp
-        L.ldpc_engine_create_ex.argtypes = [vp, i32, i32, i64, i64, i32, i32, pint]
+        L.ldpc_engine_create_ex.argtypes = [vp, i32, i32, i64, C.POINTER(Schedule), pint]
         L.ldpc_engine_create_ex.restype = vp
         L.ldpc_engine_info.argtypes = [vp, vp, vp, vp]
         L.ldpc_engine_free.argtypes = [vp]
@@ -130,7 +188,6 @@ def lib():
         L.ldpc_engine_profile.argtypes = [vp, i32]
         L.ldpc_engine_set_params.argtypes = [vp, i32, dbl, i32, C.c_uint64]
         L.ldpc_engine_stats.argtypes = [vp, C.POINTER(KernelStats)]
-        L.ldpc_engine_wall.argtypes = [vp, vp, vp]
         L.ldpc_dev_malloc.argtypes = [i32, C.c_size_t]
         L.ldpc_dev_malloc.restype = vp
         L.ldpc_dev_free.argtypes = [i32, vp]
@@ -154,19 +211,21 @@ def device_count() -> int:
 
 
 def _algo(a) -> int:
-    """ABI algorithm code of a name or of a reference decoder_type int."""
+    """ABI algorithm code of a name, an Algo member, or a reference decoder_type int."""
+    if isinstance(a, Algo):
+        return int(a)
     if isinstance(a, str):
         if a.lower() in _NAMES:
             return _NAMES[a.lower()]
     elif isinstance(a, (int, np.integer)) and not isinstance(a, bool) and int(a) in DECODER_TYPES:
         return DECODER_TYPES[int(a)]
     raise ValueError(f"unknown algorithm {a!r} (names: 'bp', 'msa', 'qmsa', 'gallager_a', 'gallager_b1', "
-                     "'gallager_b2'; ints: the reference's decoder_type 0, 1, 2, 3, 20, 21, 22)")
+                     "'gallager_b2'; Algo members; ints: the reference's decoder_type 0, 1, 2, 3, 20, 21, 22)")
 
 
 def _decoder_type(a) -> int:
     """The reference decoder_type a call runs as (result file names)."""
-    if isinstance(a, (int, np.integer)) and not isinstance(a, bool):
+    if isinstance(a, (int, np.integer)) and not isinstance(a, (bool, Algo)):
         _algo(a)
         return int(a)
     return _RESULT_TYPE[_algo(a)]
@@ -278,14 +337,15 @@ class Graph:
     def decode(self, llr: np.ndarray, max_iter: int = 200, algo="bp", post: Optional[str] = "llr",
                devices: Optional[Sequence[int]] = None, chunk: int = 0, exp_on_host: bool = True,
                host_threads: int = 0, msa_precision: int = 0, msa_step: float = 0.0, msa_offset: int = 0,
-               tie_seed: int = 0):
+               tie_seed: int = 0, schedule=None):
         """Decode a batch of LLR vectors ([B][N] or [N]) on the GPU(s).
 
         Returns (hard u8[B][N], post f64[B][N] or None, iters i32[B], valid bool[B]);
         a 1-D input returns 1-D / scalar outputs.  post: 'llr' (log of the BP
         posterior ratio / the min-sum L), 'ratio' (BP raw posterior ratio) or
         None.  msa_* / tie_seed: parameters of algo='qmsa' (0 = defaults q 6,
-        step 0.5)."""
+        step 0.5).  schedule: a Schedule or a dict of its keywords (None: the
+        library's default schedule)."""
         a = _algo(algo)
         x = np.ascontiguousarray(llr, dtype=np.float64)
         single = x.ndim == 1
@@ -310,6 +370,9 @@ class Graph:
         o.host_threads = host_threads
         o.msa_precision, o.msa_step, o.msa_offset, o.tie_seed = int(msa_precision), float(msa_step), int(msa_offset), \
             int(tie_seed)
+        sch = _schedule(schedule)
+        if sch is not None:
+            o.schedule = C.pointer(sch)
         _check(lib().ldpc_decode(self._h, _ptr(x), B, int(max_iter), a, _ptr(hard), _ptr(postv), _ptr(iters),
                                  _ptr(valid), C.byref(o)))
         valid = valid.astype(bool)
@@ -400,6 +463,17 @@ def decode_files(codeword_base: str, soft_base: str, pchk_base: str, max_iter: i
             "dec_file": "dec_" + codeword_base + ".txt", "result_file": name}
 
 
+def _schedule_kw(schedule) -> dict:
+    """Schedule / dict / None -> Schedule.make keywords."""
+    if schedule is None:
+        return {}
+    if isinstance(schedule, Schedule):
+        kw = {k: bool(schedule.flags & b) for k, b in SCHED_FLAGS.items() if schedule.flags_set & b}
+        kw.update({k: getattr(schedule, k) for k in SCHED_FIELDS if getattr(schedule, k)})
+        return kw
+    return dict(schedule)
+
+
 # ---------------------------------------------------------------------------
 # device-resident engine (bench / pipelines keeping data in HBM)
 # ---------------------------------------------------------------------------
@@ -436,34 +510,32 @@ class DeviceBuffer:
 
 
 class Engine:
-    def __init__(self, g: Graph, device: int = 0, algo="bp", chunk: int = 0, group_tiles: int = -1,
-                 nontemporal: Optional[bool] = None, pipeline: Optional[bool] = None,
-                 csc_scratch: Optional[bool] = None, continuous: Optional[bool] = None,
-                 resident: Optional[bool] = None):
+    """Device-resident decoder (ldpc_engine_*): one device, one HIP stream.
+    The schedule comes from `schedule` (a Schedule or dict) and/or the
+    keyword shortcuts (group_tiles, nontemporal, continuous, resident, ...,
+    any Schedule.make keyword); unset ones keep the library defaults."""
+
+    def __init__(self, g: Graph, device: int = 0, algo="bp", chunk: int = 0, schedule=None, **sched_kw):
         self.g, self.device, self.algo = g, device, _algo(algo)
+        kw = dict(_schedule_kw(schedule))
+        kw.update({k: v for k, v in sched_kw.items() if v is not None})
+        if kw.get("group_tiles") is not None and kw["group_tiles"] < 0:
+            kw.pop("group_tiles")  # -1: default (the ABI's 0)
+        sch = Schedule.make(**kw)
         err = C.c_int(0)
-        flags_set = flags = 0
-        for bit, v in zip((0, 1, 2, 3, 5), (nontemporal, pipeline, csc_scratch, continuous, resident)):
-            if v is not None:
-                flags_set |= 1 << bit
-                flags |= int(bool(v)) << bit
-        self._h = lib().ldpc_engine_create_ex(g.handle, device, self.algo, chunk, group_tiles, flags_set, flags,
-                                              C.byref(err))
+        self._h = lib().ldpc_engine_create_ex(g.handle, device, self.algo, chunk, C.byref(sch), C.byref(err))
         if not self._h:
             raise LdpcError(err.value, (lib().ldpc_last_error() or b"").decode())
         cap, grp, fl = C.c_int64(), C.c_int64(), C.c_int32()
         _check(lib().ldpc_engine_info(self._h, C.byref(cap), C.byref(grp), C.byref(fl)))
-        self.cap, self.group_tiles = cap.value, grp.value
-        self.nontemporal, self.pipeline, self.csc_scratch = bool(fl.value & 1), bool(fl.value & 2), bool(fl.value & 4)
-        self.continuous = bool(fl.value & 8)
-        self.msa_compressed = bool(fl.value & 16)  # min-sum c2v as per-row records + per-edge codes
-        self.resident = bool(fl.value & 32)  # in-place pool of a few tiles (LDPC_RES)
-        self.syndrome_split = bool(fl.value & 64)  # multi-block continuous-mode syndrome (LDPC_SYN_SPLIT)
-        self.syndrome_fused = bool(fl.value & 128)  # syndrome in the grouped check launches (LDPC_SYN_FUSED)
-        self.tile_streams = bool(fl.value & 256)  # resident pool, one stream per tile (LDPC_RES_STREAMS)
-        self.pingpong = bool(fl.value & 512)  # resident BP pool, check(t) + variable(t-1) per launch (LDPC_PINGPONG)
-        self.xcd_resident = bool(fl.value & 1024)  # one persistent launch, slots in the XCDs' L2 (LDPC_XR)
-        self.msa_meta = bool(fl.value & 2048)  # MSA-C without per-edge codes: 16-bit meta word per row (LDPC_MSA_META)
+        self.cap, self.group_tiles, self.flags = cap.value, grp.value, fl.value
+        f = fl.value
+        self.nontemporal = bool(f & SCHED_FLAGS["nontemporal"])
+        self.continuous = bool(f & SCHED_FLAGS["continuous"])
+        self.msa_compressed = bool(f & SCHED_FLAGS["msa_compressed"])  # min-sum c2v as per-row records + meta words
+        self.resident = bool(f & SCHED_FLAGS["resident"])  # in-place pool of a few tiles
+        self.syndrome_split = bool(f & SCHED_FLAGS["split_syndrome"])  # multi-block continuous-mode syndrome
+        self.first_from_prior = bool(f & SCHED_FLAGS["first_from_prior"])
 
     def decode(self, d_in, in_kind: int, B: int, max_iter: int, d_hard=None, d_post=None, post_kind=POST_LLR,
                d_iters=None, d_valid=None):
@@ -483,12 +555,6 @@ class Engine:
     def profile(self, stride: int):
         """HIP-event timing of every `stride`-th launch per kernel class (0: off)."""
         _check(lib().ldpc_engine_profile(self._h, int(stride)))
-
-    def wall(self):
-        """(ms, runs): device time of whole decodes with concurrent tile streams."""
-        ms, runs = C.c_double(), C.c_int64()
-        _check(lib().ldpc_engine_wall(self._h, C.byref(ms), C.byref(runs)))
-        return ms.value, runs.value
 
     def stats(self) -> dict:
         s = KernelStats()

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LDPC_AMD_ABI_VERSION 1
+#define LDPC_AMD_ABI_VERSION 2
 
 /* error codes */
 enum {
@@ -71,6 +71,46 @@ enum {
 
 typedef struct ldpc_graph ldpc_graph;
 
+/* Decode schedule.  The schedule changes only which
+ * codewords share a launch and where messages live between the phases, never
+ * a codeword's arithmetic: every schedule is bit-exact.  A zeroed struct (or
+ * a NULL pointer) selects the defaults, which were chosen by same-process A/B
+ * measurements on MI355X.  The library reads no environment variable to pick
+ * a schedule. */
+enum {
+    LDPC_SCHED_NONTEMPORAL = 1 << 0,    /* grouped schedule: nontemporal variable->check stream (default on) */
+    LDPC_SCHED_CONTINUOUS = 1 << 3,     /* continuous batching: a finished codeword's lane is refilled with
+                                           the next one (fp64 decoders on (8,72)-regular graphs; default on;
+                                           needs hard / iters / valid outputs) */
+    LDPC_SCHED_MSA_COMPRESSED = 1 << 4, /* min-sum check->variable messages as per-row records (min1, min2,
+                                           NaN planes) + one 32-bit meta word per row (default on) */
+    LDPC_SCHED_RESIDENT = 1 << 5,       /* continuous BP / fp64 min-sum: a pool of pool_tiles tiles iterated
+                                           in place, its state sized to the 256 MB Infinity Cache, the
+                                           syndrome fused into the check kernel (default on when the lane
+                                           pool is chosen by the engine or is at most 4 tiles) */
+    LDPC_SCHED_SPLIT_SYNDROME = 1 << 6, /* (ldpc_engine_info only) continuous grouped schedule: syndrome
+                                           spread over syn_blocks blocks per tile */
+    LDPC_SCHED_FIRST_FROM_PRIOR = 1 << 12, /* single-fill BP decodes: the first check derives its messages
+                                              from the prior instead of E stored copies (default on) */
+    LDPC_SCHED_LR_TABLE = 1 << 13,      /* ldpc_decode, BP with host exp: LLR batches on a k * unit lattice
+                                           cross PCIe as one byte each + a table of host exp(k * unit)
+                                           (default on; off = host exp of every value) */
+    LDPC_SCHED_DEBUG_NO_DRAIN = 1 << 14 /* tests only: the host ignores a drained pool, so a decode runs
+                                           into its step bound and returns LDPC_ERR_DEVICE (default off) */
+};
+
+typedef struct ldpc_schedule {
+    int32_t flags_set;   /* LDPC_SCHED_* bits whose value is taken from `flags`; the others keep the default */
+    int32_t flags;
+    int32_t group_tiles; /* grouped schedule: 64-codeword tiles per check/variable launch
+                            (0 = default: 3, 4 for compressed min-sum; < 0 = the whole pass) */
+    int32_t var_cpw;     /* columns per variable-phase wavefront: 1, 2, 4 or 8 (0 = default 4) */
+    int32_t pool_tiles;  /* resident pool tiles when the engine chooses the pool (0 = default 3) */
+    int32_t poll_every;  /* resident pool: steps between occupancy polls (0 = default 8) */
+    int32_t syn_blocks;  /* continuous grouped schedule: syndrome blocks per tile (0 = default 32) */
+    int32_t reserved;    /* 0 */
+} ldpc_schedule;
+
 typedef struct ldpc_opts {
     int32_t n_devices;      /* <= 0: use device 0 only */
     const int32_t *devices; /* device ordinals (NULL: 0..n_devices-1) */
@@ -87,6 +127,7 @@ typedef struct ldpc_opts {
     int32_t reserved0;
     double msa_step;        /* LDPC_ALGO_QMSA: quantizer step (g_step_length), > 0 */
     uint64_t tie_seed;      /* LDPC_ALGO_QMSA: seed of the zero-posterior tie hash */
+    const ldpc_schedule *schedule; /* NULL: the default schedule (ABI version 2) */
 } ldpc_opts;
 
 /* ------------------------------------------------------------------------ */
@@ -130,11 +171,12 @@ int ldpc_graph_info(const ldpc_graph *g, int32_t *M, int32_t *N, int64_t *E, int
 
 /* Block structure of array codes (RS-LDPC, quasi-cyclic): H is row_blocks x
  * col_blocks permutation matrices of size Q, rows in contiguous blocks.  Q = 0
- * when H has no such structure (then only the tiled decoders run).
+ * when H has no such structure (regular degrees, M = dv * Q, N = dc * Q).
  * col_block[N] (may be NULL) receives each column's block.  The column blocks
  * are found as contiguous runs of Q columns or, for RS-LDPC codes with
  * permuted columns (the DNA code), by matching the column row sets against
- * ldpc_graph_rs_ldpc(log2 Q, col_blocks, row_blocks). */
+ * ldpc_graph_rs_ldpc(log2 Q, col_blocks, row_blocks).  Code-structure tooling;
+ * the decoders do not depend on it. */
 int ldpc_graph_blocks(const ldpc_graph *g, int32_t *Q, int32_t *row_blocks, int32_t *col_blocks,
                       int32_t *col_block);
 
@@ -168,23 +210,13 @@ int ldpc_decode(const ldpc_graph *g, const double *llr, int64_t B, int32_t max_i
 /* ------------------------------------------------------------------------ */
 typedef struct ldpc_engine ldpc_engine;
 
-/* One engine = one device + one HIP stream + chunk-sized message buffers. */
+/* One engine = one device + one HIP stream + chunk-sized message buffers,
+ * with the default schedule. */
 ldpc_engine *ldpc_engine_create(const ldpc_graph *g, int32_t device, int32_t algo, int64_t chunk, int *err);
 
-/* Same with the schedule knobs: group_tiles = 64-codeword tiles per
- * check/variable launch (the check->variable messages of one group stay
- * resident in the Infinity Cache; 0 = whole pass, -1 = default / env
- * LDPC_GROUP_TILES).  Schedule flags: the bits set in flags_set are taken
- * from flags, the others from the defaults / environment.
- * Bit 0 = nontemporal v2c stream, bit 1 = overlap
- * check(g+1) with variable(g) on a second stream, bit 2 = check->variable
- * messages stored in column order, bit 3 = continuous batching (a finished
- * codeword's lane is refilled with the next one; needs hard/iters/valid
- * outputs), bit 5 = resident pool (continuous BP / fp64 min-sum: a pool of
- * LDPC_RES_TILES tiles iterated in place, sized for the Infinity Cache)
- * (env LDPC_NT_D, LDPC_PIPE, LDPC_LR_CSC, LDPC_CONT, LDPC_RES). */
+/* Same with an explicit schedule (NULL = defaults). */
 ldpc_engine *ldpc_engine_create_ex(const ldpc_graph *g, int32_t device, int32_t algo, int64_t chunk,
-                                   int64_t group_tiles, int32_t flags_set, int32_t flags, int *err);
+                                   const ldpc_schedule *schedule, int *err);
 void ldpc_engine_free(ldpc_engine *e);
 
 /* Decode B codewords whose input already lives in device memory (d_in:
@@ -224,24 +256,10 @@ int ldpc_engine_profile(ldpc_engine *e, int32_t stride);
 int ldpc_engine_set_params(ldpc_engine *e, int32_t msa_precision, double msa_step, int32_t msa_offset,
                            uint64_t tie_seed);
 /* The schedule an engine runs with: resident codewords per pass (the lane
- * pool in continuous mode), group tiles, and flags with the bits of
- * ldpc_engine_create_ex plus bit 4 = compressed min-sum check->variable
- * messages (env LDPC_MSA_C); bit 5 as in create_ex; bit 6 =
- * continuous-mode syndrome spread over several blocks per tile (env
- * LDPC_SYN_SPLIT); bit 7 = syndrome fused into the grouped check launches
- * (env LDPC_SYN_FUSED); bit 8 = resident pool with one HIP stream per pool
- * tile (env LDPC_RES_STREAMS; the tiles' kernels run concurrently); bit 9 =
- * resident BP pool, ping-pong launches (env LDPC_PINGPONG); bit 10 = the
- * XCD-resident BP decoder for array codes (env LDPC_XR);
- * bit 11 = compressed min-sum without per-edge codes: one 16-bit meta word per row,
- * sign bits kept by the variable phase (env LDPC_MSA_META). */
+ * pool in continuous mode), tiles per launch, and the LDPC_SCHED_* bits that
+ * are in effect. */
 int ldpc_engine_info(ldpc_engine *e, int64_t *cap, int64_t *group_tiles, int32_t *flags);
 int ldpc_engine_stats(ldpc_engine *e, ldpc_kernel_stats *out);
-/* Device time of whole decodes with concurrent tile streams (bit 8 of
- * ldpc_engine_info): HIP events on the engine stream around each decode
- * while profiling is on (ldpc_engine_profile resets it).  Their kernels
- * overlap, so per-launch durations do not add up to the decode's time. */
-int ldpc_engine_wall(ldpc_engine *e, double *ms, int64_t *runs);
 
 /* Device buffers for callers without their own HIP allocator (bench, tests). */
 enum { LDPC_H2D = 0, LDPC_D2H = 1, LDPC_D2D = 2 };

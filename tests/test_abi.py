@@ -27,7 +27,7 @@ def test_exports_match_header(L):
     lib = L.lib()
     for name in declared:
         assert hasattr(lib, name)
-    assert lib.ldpc_abi_version() == 1
+    assert lib.ldpc_abi_version() == 2 == L.ABI_VERSION
 
 
 def test_graph_load_matches_oracle(L, og):
@@ -116,8 +116,31 @@ def test_algo_ints_are_reference_decoder_types(L):
     for bad in (4, 5, 10, 50, True, "gallager", 1.0):
         with pytest.raises(ValueError):
             L._algo(bad)
+    # the module's own ABI constants are Algo members: they select their decoder,
+    # never the decoder_type with the same number (ALGO_MSA == 1 is not Gallager A)
+    for a in L.Algo:
+        assert L._algo(a) == int(a)
+    assert L._algo(L.ALGO_MSA) == 1 and L._algo(L.ALGO_QMSA) == 2 and L._algo(L.ALGO_GALLAGER_B2) == 5
     # result file names carry the decoder_type the call ran as
     assert [L._decoder_type(a) for a in ("bp", "msa", "gallager_a", 1, 21, "qmsa")] == [0, 20, 1, 1, 21, 21]
+    assert [L._decoder_type(a) for a in (L.ALGO_BP, L.ALGO_MSA, L.ALGO_GALLAGER_A)] == [0, 20, 1]
+
+
+def test_schedule_struct_matches_header(L):
+    """ldpc_schedule / ldpc_opts layouts of the ctypes shim against the
+    header (ABI version 2), and Schedule.make's keyword mapping."""
+    import ctypes as C
+    hdr = open(os.path.join(ROOT, "include", "ldpc_amd.h")).read()
+    for name, bit in L.SCHED_FLAGS.items():
+        m = re.search(r"LDPC_SCHED_" + name.upper() + r"\s*=\s*1\s*<<\s*(\d+)", hdr)
+        assert m and (1 << int(m.group(1))) == bit, name
+    assert C.sizeof(L.Schedule) == 32 and C.sizeof(L.Opts) == 72
+    s = L.Schedule.make(resident=False, continuous=True, group_tiles=2, syn_blocks=7)
+    assert s.flags_set == L.SCHED_FLAGS["resident"] | L.SCHED_FLAGS["continuous"]
+    assert s.flags == L.SCHED_FLAGS["continuous"] and s.group_tiles == 2 and s.syn_blocks == 7
+    with pytest.raises(TypeError):
+        L.Schedule.make(pingpong=True)
+    assert L._schedule_kw(s) == {"resident": False, "continuous": True, "group_tiles": 2, "syn_blocks": 7}
 
 
 def test_cli_rejects_bad_argc():
@@ -162,8 +185,8 @@ def test_graph_blocks_array_structure(L):
     """ldpc_graph_blocks: the DNA code is RS-LDPC(8, 72, 8) with permuted
     columns; its column blocks are found by row-set matching and equal the RS
     blocks of the committed column permutation (tests/golden/code_fixtures.npz).
-    Codes built in natural order get contiguous blocks; graphs without the
-    structure (irregular, Q < 64) report none."""
+    Codes built in natural order get contiguous blocks (any Q); graphs without
+    the structure (irregular) report none."""
     from conftest import GOLDEN
     G = L.Graph(PCHK)
     Q, rb, cb, cls = G.blocks()
@@ -176,6 +199,7 @@ def test_graph_blocks_array_structure(L):
     R = L.Graph.rs_ldpc(7, 72, 8)
     Q, rb, cb, cls = R.blocks()
     assert (Q, rb, cb) == (128, 8, 72) and np.array_equal(cls, np.arange(R.N) // 128)
-    assert L.Graph.rs_ldpc(5, 16, 4).blocks() is None  # Q = 32
+    Q, rb, cb, cls = L.Graph.rs_ldpc(5, 16, 4).blocks()
+    assert (Q, rb, cb) == (32, 4, 16) and np.array_equal(cls, np.arange(16 * 32) // 32)
     irr = L.Graph.from_edges(4, 6, [0, 0, 1, 1, 2, 3], [0, 1, 2, 3, 4, 5])
     assert irr.blocks() is None

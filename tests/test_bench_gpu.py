@@ -28,7 +28,7 @@ def _bench(*args):
 @pytest.mark.parametrize("algo,p", [("bp", 0.02), ("msa", 0.002)])
 def test_bench_bsc_line(gpu, algo, p):
     out = _bench("--algo", algo, "--p", str(p), "--batch-per-gpu", "2048", "--steps", "1", "--warmup", "1",
-                 "--cpu-seconds", "1")
+                 "--cpu-seconds", "1", "--secondary", "0")
     assert out["steps"] == 1 and out["dtype"] == "f64"
     rl = out["roofline"]
     assert rl["bound"] == "hbm" and rl["unit"] == "GB/s" and rl["peak"] == 8000.0
@@ -37,6 +37,23 @@ def test_bench_bsc_line(gpu, algo, p):
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["per_core"] > 0
     if algo == "bp":
         assert out["config"]["mean_iters"] == 50.0
+    ck = out["check"]
+    assert ck["mismatches"] == 0 and ck["checked"] >= 16 and len(ck["per_rank"]) == 1
+    assert rl["kernel"] in rl["kernels"].values()
+
+
+def test_bench_secondary_legs(gpu):
+    """The driver-run line's secondary legs (config 5 min-sum, config 2 DNA
+    batch through the host API), shrunk: each has its own oracle check."""
+    out = _bench("--batch-per-gpu", "1024", "--steps", "1", "--warmup", "0", "--cpu-seconds", "0.5",
+                 "--msa-batch", "8192")
+    sec = out["secondary"]
+    m = sec["config5_msa_1m"]
+    assert m["batch"] == 8192 and m["compressed_msa"] and m["check"]["mismatches"] == 0 and m["check"]["checked"] >= 8
+    assert m["roofline"]["kernel"].startswith("k_var_msa_c") and m["roofline"]["achieved"] > 0
+    d = sec["config2_dna272"]
+    assert d["genie_ok"] == 272 and d["check"]["mismatches"] == 0 and d["check"]["checked"] == 272
+    assert d["host_api_ms_median"] > 0
 
 
 def test_bench_dna272_line(gpu):

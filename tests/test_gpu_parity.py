@@ -267,73 +267,67 @@ def test_multi_device_api_single_gpu_box(G, og, codewords):
     _cmp(G, og, llr, 20, devices=[0, 0])
 
 
-@pytest.mark.parametrize("group,nt,pipe,csc,cont", [(1, 0, 0, 0, 0), (1, 1, 1, 1, 0), (3, 0, 1, 0, 0), (2, 1, 0, 1, 0),
-                                                     (0, 1, 0, 0, 0), (0, 0, 0, 1, 0), (3, 1, 0, 0, 1), (1, 0, 0, 1, 1),
-                                                     (0, 1, 0, 0, 1)])
-def test_grouped_schedules_bitexact(gpu, og, codewords, monkeypatch, group, nt, pipe, csc, cont):
+@pytest.mark.parametrize("group,nt,cont", [(1, 0, 0), (3, 1, 0), (2, 0, 0), (-1, 1, 0), (-1, 0, 0), (3, 1, 1),
+                                           (1, 0, 1), (-1, 1, 1)])
+def test_grouped_schedules_bitexact(gpu, og, codewords, group, nt, cont):
     """The Infinity-Cache-resident schedule (check->variable messages of one
-    tile group at a time) and the nontemporal d-stream change only the launch
-    order across codewords, never a codeword's arithmetic."""
-    monkeypatch.setenv("LDPC_GROUP_TILES", str(group))
-    monkeypatch.setenv("LDPC_NT_D", str(nt))
-    monkeypatch.setenv("LDPC_PIPE", str(pipe))
-    monkeypatch.setenv("LDPC_LR_CSC", str(csc))
-    monkeypatch.setenv("LDPC_CONT", str(cont))
-    G2 = gpu.Graph(PCHK)  # fresh graph -> fresh engine pool reads the env
+    tile group at a time; group -1 = the whole pass), the nontemporal
+    d-stream and continuous batching change only the launch order across
+    codewords, never a codeword's arithmetic."""
+    sch = dict(group_tiles=group, nontemporal=bool(nt), continuous=bool(cont), resident=False)
+    G2 = gpu.Graph(PCHK)
     llr = synth.dna_like_llrs(codewords, seed=1, reads=57000)[:200]
-    _cmp(G2, og, llr, 60)
+    _cmp(G2, og, llr, 60, schedule=sch)
     llr = synth.bsc_llrs(codewords, 0, 200, seed=2026, p=0.002)
-    _cmp(G2, og, llr, 30, algo="msa")
+    _cmp(G2, og, llr, 30, algo="msa", schedule=sch)
 
 
-@pytest.mark.parametrize("cpw,cont", [(2, 0), (4, 1), (8, 0), (2, 1)])
-def test_variable_columns_per_wave_bitexact(gpu, og, codewords, monkeypatch, cpw, cont):
+@pytest.mark.parametrize("cpw,cont", [(1, 1), (2, 0), (4, 1), (8, 0), (2, 1)])
+def test_variable_columns_per_wave_bitexact(gpu, og, codewords, cpw, cont):
     """k_var_m (CPW columns per wave, BP and min-sum) changes only which
     wave handles a column, never a column's arithmetic; with continuous
     batching its refill path initialises fresh lanes."""
-    monkeypatch.setenv("LDPC_VAR_CPW", str(cpw))
-    monkeypatch.setenv("LDPC_CONT", str(cont))
+    sch = dict(var_cpw=cpw, continuous=bool(cont), resident=False, msa_compressed=False)
     G2 = gpu.Graph(PCHK)
     llr = synth.dna_like_llrs(codewords, seed=3, reads=57000)[:200]
-    _cmp(G2, og, llr, 60)
+    _cmp(G2, og, llr, 60, schedule=sch)
     llr = synth.bsc_llrs(codewords, 0, 150, seed=7, p=0.004)
-    _cmp(G2, og, llr, 40)
+    _cmp(G2, og, llr, 40, schedule=sch)
     llr = synth.bsc_llrs(codewords, 0, 200, seed=8, p=0.002)
-    _cmp(G2, og, llr, 30, algo="msa")
+    _cmp(G2, og, llr, 30, algo="msa", schedule=sch)
 
 
-@pytest.mark.parametrize("res,tiles,poll,cpw", [(1, 2, 4, 4), (1, 1, 1, 4), (1, 3, 2, 2), (1, 2, 7, 1), (0, 2, 4, 4)])
-def test_resident_pool_in_place_bitexact(gpu, og, codewords, monkeypatch, res, tiles, poll, cpw):
-    """Resident pool (engine.hip run_cont `res`, kernels.hpp k_syndrome_res):
-    a pool of 1-3 tiles iterated in place (check->variable messages written
-    over the variable->check messages of the same edges), the syndrome spread
-    over several blocks per tile with last-block lane bookkeeping, occupancy
-    polled every `poll` steps.  BP and fp64 min-sum stay bit-exact across
-    mixed early exits, all lanes finishing at once (p = 0.02, exactly 50
-    iterations), max_iter 0, batches smaller than the pool, NaN / inf inputs."""
-    monkeypatch.setenv("LDPC_RES", str(res))
-    monkeypatch.setenv("LDPC_RES_TILES", str(tiles))
-    monkeypatch.setenv("LDPC_RES_POLL", str(poll))
-    monkeypatch.setenv("LDPC_VAR_CPW", str(cpw))
-    monkeypatch.setenv("LDPC_MSA_C", "0")
-    monkeypatch.setenv("LDPC_CONT", "1")
+@pytest.mark.parametrize("tiles,poll,cpw", [(2, 4, 4), (1, 1, 4), (3, 2, 2), (2, 7, 1)])
+def test_resident_pool_in_place_bitexact(gpu, og, codewords, tiles, poll, cpw):
+    """Resident pool (engine.hip run_cont `res`, k_check_bp / k_check_msa with
+    RES): a pool of 1-3 tiles iterated in place (check->variable messages
+    written over the variable->check messages of the same edges), the
+    syndrome fused into the check kernel with last-block lane bookkeeping,
+    occupancy polled every `poll` steps.  BP and fp64 min-sum stay bit-exact
+    across mixed early exits, all lanes finishing at once (p = 0.02, exactly
+    50 iterations), max_iter 0, batches smaller than the pool, NaN / inf."""
+    sch = dict(resident=True, pool_tiles=tiles, poll_every=poll, var_cpw=cpw, msa_compressed=False)
     G2 = gpu.Graph(PCHK)
+    kw = dict(chunk=64 * tiles, schedule=sch)
+    e = gpu.Engine(G2, 0, "bp", **kw)
+    assert e.resident and not e.syndrome_split
+    del e
     llr = synth.dna_like_llrs(codewords, seed=1, reads=57000)[:200]
-    _cmp(G2, og, llr, 60, chunk=64 * tiles)
+    _cmp(G2, og, llr, 60, **kw)
     llr = np.concatenate([synth.bsc_llrs(codewords, 0, 150, seed=3, p=0.003),
                           synth.bsc_llrs(codewords, 150, 130, seed=2026, p=0.02)])
-    _, _, it, _ = _cmp(G2, og, llr, 50, chunk=64 * tiles)
+    _, _, it, _ = _cmp(G2, og, llr, 50, **kw)
     assert (it[150:] == 50).all() and len(np.unique(it[:150])) > 2
-    _cmp(G2, og, llr[:70], 0, chunk=64 * tiles)
-    _cmp(G2, og, llr[:5], 50, chunk=64 * tiles)
-    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 200, seed=8, p=0.002), 30, algo="msa", chunk=64 * tiles)
+    _cmp(G2, og, llr[:70], 0, **kw)
+    _cmp(G2, og, llr[:5], 50, **kw)
+    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 200, seed=8, p=0.002), 30, algo="msa", **kw)
     rng = np.random.default_rng(21)
     llr = synth.dna_like_llrs(codewords, seed=2, reads=60000)[:100]
     llr[rng.random(llr.shape) < 0.002] = np.nan
     llr[rng.random(llr.shape) < 0.002] = np.inf
     llr[rng.random(llr.shape) < 0.002] = -np.inf
     ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 40, algo=0, post_mode=1, threads=8)
-    h, p, it, v = G2.decode(llr, max_iter=40, algo="bp", post="ratio", chunk=64 * tiles)
+    h, p, it, v = G2.decode(llr, max_iter=40, algo="bp", post="ratio", **kw)
     assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
     nan = np.isnan(ref_p)
     assert np.array_equal(np.isnan(p), nan)
@@ -341,42 +335,39 @@ def test_resident_pool_in_place_bitexact(gpu, og, codewords, monkeypatch, res, t
 
 
 @pytest.mark.parametrize("chunk", [64, 128])
-def test_continuous_batching_edge_cases(gpu, og, codewords, monkeypatch, chunk):
+def test_continuous_batching_edge_cases(gpu, og, codewords, chunk):
     """Continuous mode with a pool smaller than the batch (lanes are refilled
     many times), mixed early exits, max_iter 0, B not a multiple of 64, and
     the posterior written at each codeword's own exit."""
-    monkeypatch.setenv("LDPC_CONT", "1")
     G2 = gpu.Graph(PCHK)
+    sch = dict(continuous=True)
     llr = np.concatenate([synth.bsc_llrs(codewords, 0, 150, seed=3, p=0.003),
                           synth.bsc_llrs(codewords, 150, 50, seed=3, p=0.02)])
-    _cmp(G2, og, llr, 25, chunk=chunk)
-    _cmp(G2, og, llr[:70], 0, chunk=chunk)
-    _cmp(G2, og, llr[:130], 12, algo="msa", chunk=chunk)
+    _cmp(G2, og, llr, 25, chunk=chunk, schedule=sch)
+    _cmp(G2, og, llr[:70], 0, chunk=chunk, schedule=sch)
+    _cmp(G2, og, llr[:130], 12, algo="msa", chunk=chunk, schedule=sch)
 
 
-@pytest.mark.parametrize("msa_c,group,cont,cpw,meta", [(0, 3, 1, 4, 1), (1, 1, 0, 1, 1), (1, 2, 1, 2, 1), (1, 3, 0, 4, 1),
-                                                       (1, 8, 1, 4, 1), (1, 0, 0, 2, 1), (1, 2, 1, 8, 1), (1, 3, 0, 4, 0),
-                                                       (1, 8, 1, 4, 0)])
-def test_min_sum_compressed_messages_bitexact(gpu, og, codewords, monkeypatch, msa_c, group, cont, cpw, meta):
+@pytest.mark.parametrize("msa_c,group,cont,cpw", [(0, 3, 1, 4), (1, 1, 0, 1), (1, 2, 1, 2), (1, 3, 0, 4),
+                                                  (1, 8, 1, 4), (1, -1, 0, 2), (1, 4, 1, 4), (1, 5, 1, 1)])
+def test_min_sum_compressed_messages_bitexact(gpu, og, codewords, msa_c, group, cont, cpw):
     """MSA-C (kernels.hpp k_check_msa_c / k_var_msa_c): the check phase stores
-    per row the four magnitudes min1 / min2 / |x_0| / |x_1| and either per edge
-    a sign + source code (meta 0) or per row one 16-bit meta word (sign parity,
-    NaN at x_0 / x_1, index of min1) while the variable phase keeps the sign
-    bits of the v2c it stored (meta 1, an option); the
-    variable phase rebuilds each c2v by the reference's expression, so hard
-    bits, iterations, valid flags and the posterior L stay bit-exact -- across
-    group sizes (XCD-affine tile order), continuous batching, columns per wave,
-    and the NaN / inf / -0.0 first-other-edge cases."""
-    monkeypatch.setenv("LDPC_MSA_C", str(msa_c))
-    monkeypatch.setenv("LDPC_MSA_META", str(meta))
-    monkeypatch.setenv("LDPC_GROUP_TILES", str(group))
-    monkeypatch.setenv("LDPC_CONT", str(cont))
-    monkeypatch.setenv("LDPC_VAR_CPW", str(cpw))
+    per row a {min1, min2} record, a 32-bit meta word (sign parity, NaN at
+    x_0 / x_1, edge id of min1) and the NaN planes when needed; the variable
+    phase rebuilds each c2v from them and the sign bits of the v2c it stored,
+    so hard bits, iterations, valid flags and the posterior L stay bit-exact
+    -- across group sizes (XCD-affine tile order, groups that do not divide
+    8), continuous batching, columns per wave, and the NaN / inf / -0.0
+    first-other-edge cases."""
+    sch = dict(msa_compressed=bool(msa_c), group_tiles=group, continuous=bool(cont), var_cpw=cpw)
     G2 = gpu.Graph(PCHK)
+    e = gpu.Engine(G2, 0, "msa", schedule=sch)
+    assert e.msa_compressed == bool(msa_c)
+    del e
     llr = synth.bsc_llrs(codewords, 0, 300, seed=2026, p=0.002)
-    _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa")
+    _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", schedule=sch)
     assert len(np.unique(it)) > 2
-    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 70, seed=5, p=0.01), 12, algo="msa")
+    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 70, seed=5, p=0.01), 12, algo="msa", schedule=sch)
     rng = np.random.default_rng(13)
     llr = synth.bsc_llrs(codewords, 0, 130, seed=11, p=0.004)
     llr[rng.random(llr.shape) < 0.003] = np.nan
@@ -385,207 +376,46 @@ def test_min_sum_compressed_messages_bitexact(gpu, og, codewords, monkeypatch, m
     llr[rng.random(llr.shape) < 0.01] = -0.0
     llr[:2] = np.nan
     ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 20, algo=1, post_mode=0, threads=8)
-    h, p, it, v = G2.decode(llr, max_iter=20, algo="msa", post="llr")
+    h, p, it, v = G2.decode(llr, max_iter=20, algo="msa", post="llr", schedule=sch)
     assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
     nan = np.isnan(ref_p)
     assert np.array_equal(np.isnan(p), nan)
     assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64))
 
 
-@pytest.mark.parametrize("tiles,poll,cpw", [(2, 4, 4), (1, 1, 2), (3, 2, 4), (4, 7, 1)])
-def test_min_sum_compressed_resident_pool_bitexact(gpu, og, codewords, monkeypatch, tiles, poll, cpw):
-    """Resident pool for compressed min-sum (LDPC_RES_MSA_C): k_check_msa_c
-    with the fused syndrome + last-block lane bookkeeping (SYN), k_var_msa_c
-    writing the finished lanes' hard bits / posterior before refilling them.
-    Bit-exact across pool sizes (1-4 tiles, the XCD-affine order with and
-    without gt | 8), poll intervals, mixed exits, non-converging lanes,
-    max_iter 0, batches smaller than the pool and NaN / inf / -0.0 inputs."""
-    monkeypatch.setenv("LDPC_MSA_C", "1")
-    monkeypatch.setenv("LDPC_RES_MSA_C", "1")
-    monkeypatch.setenv("LDPC_RES_TILES_MSA_C", str(tiles))
-    monkeypatch.setenv("LDPC_RES_POLL", str(poll))
-    monkeypatch.setenv("LDPC_VAR_CPW", str(cpw))
-    monkeypatch.setenv("LDPC_CONT", "1")
-    G2 = gpu.Graph(PCHK)
-    llr = synth.bsc_llrs(codewords, 0, 300, seed=2026, p=0.002)
-    _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", chunk=64 * tiles)
-    assert len(np.unique(it)) > 2
-    _cmp(G2, og, synth.bsc_llrs(codewords, 0, 70, seed=5, p=0.01), 12, algo="msa", chunk=64 * tiles)
-    _cmp(G2, og, llr[:70], 0, algo="msa", chunk=64 * tiles)
-    _cmp(G2, og, llr[:5], 50, algo="msa", chunk=64 * tiles)
-    rng = np.random.default_rng(17)
-    llr = synth.bsc_llrs(codewords, 0, 130, seed=11, p=0.004)
-    llr[rng.random(llr.shape) < 0.003] = np.nan
-    llr[rng.random(llr.shape) < 0.002] = np.inf
-    llr[rng.random(llr.shape) < 0.002] = -np.inf
-    llr[rng.random(llr.shape) < 0.01] = -0.0
-    llr[:2] = np.nan
-    ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 20, algo=1, post_mode=0, threads=8)
-    h, p, it, v = G2.decode(llr, max_iter=20, algo="msa", post="llr", chunk=64 * tiles)
-    assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
-    nan = np.isnan(ref_p)
-    assert np.array_equal(np.isnan(p), nan)
-    assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64))
-
-
-@pytest.mark.parametrize("algo,msa_c,group,chunk", [("bp", 0, 3, 256), ("bp", 0, 1, 128), ("msa", 1, 4, 512),
-                                                    ("msa", 1, 2, 128), ("msa", 0, 3, 192)])
-def test_fused_syndrome_grouped_bitexact(gpu, og, codewords, monkeypatch, algo, msa_c, group, chunk):
-    """LDPC_SYN_FUSED (engine.hip run_cont `syn_fused`): the grouped
-    continuous schedule with each group's check launch computing the
-    syndrome of its tiles and the lane bookkeeping (ResStep), and the
-    variable launch writing finished codewords' outputs before the refill.
-    Pools smaller than the batch (many refills), groups that do not divide
-    the pool, mixed exits, max_iter 0, posterior at each codeword's exit."""
-    monkeypatch.setenv("LDPC_SYN_FUSED", "1")
-    monkeypatch.setenv("LDPC_CONT", "1")
-    monkeypatch.setenv("LDPC_RES", "0")
-    monkeypatch.setenv("LDPC_RES_MSA_C", "0")
-    monkeypatch.setenv("LDPC_MSA_C", str(msa_c))
-    monkeypatch.setenv("LDPC_GROUP_TILES", str(group))
+@pytest.mark.parametrize("algo,msa_c,group,chunk,blocks", [("msa", 1, 4, 1024, 16), ("msa", 1, 2, 128, 3),
+                                                           ("msa", 0, 3, 192, 64), ("bp", 0, 3, 256, 8),
+                                                           ("bp", 0, 1, 128, 1)])
+def test_split_syndrome_bitexact(gpu, og, codewords, algo, msa_c, group, chunk, blocks):
+    """The continuous grouped schedule's syndrome (kernels.hpp
+    k_syndrome_split) spread over `blocks` blocks per tile (8 rows per wave, 8
+    edge parts per row), the last block per tile running the lane bookkeeping
+    and the variable launch writing the finished codewords' outputs."""
+    sch = dict(syn_blocks=blocks, continuous=True, resident=False, msa_compressed=bool(msa_c), group_tiles=group)
     G2 = gpu.Graph(PCHK)
     if algo == "bp":
         llr = np.concatenate([synth.bsc_llrs(codewords, 0, 300, seed=3, p=0.003),
                               synth.bsc_llrs(codewords, 300, 100, seed=2026, p=0.02)])
-        _, _, it, _ = _cmp(G2, og, llr, 30, chunk=chunk)
-        llr = synth.dna_like_llrs(codewords, seed=1, reads=57000)[:150]
-        _cmp(G2, og, llr, 60, chunk=chunk)
+        _, _, it, _ = _cmp(G2, og, llr, 30, chunk=chunk, schedule=sch)
     else:
         llr = synth.bsc_llrs(codewords, 0, 400, seed=2026, p=0.002)
-        _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", chunk=chunk)
+        _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", chunk=chunk, schedule=sch)
     assert len(np.unique(it)) > 2
-    _cmp(G2, og, llr[:70], 0, algo=algo, chunk=chunk)
-    _cmp(G2, og, llr[:3], 20, algo=algo, chunk=chunk)
+    _cmp(G2, og, llr[:70], 0, algo=algo, chunk=chunk, schedule=sch)
+    _cmp(G2, og, llr[:3], 20, algo=algo, chunk=chunk, schedule=sch)
 
 
-@pytest.mark.parametrize("algo,msa_c,group,chunk,split", [("msa", 1, 4, 1024, 16), ("msa", 1, 2, 128, 3),
-                                                          ("msa", 0, 3, 192, 64), ("bp", 0, 3, 256, 8),
-                                                          ("bp", 0, 1, 128, 1)])
-def test_split_syndrome_bitexact(gpu, og, codewords, monkeypatch, algo, msa_c, group, chunk, split):
-    """LDPC_SYN_SPLIT (kernels.hpp k_syndrome_split): the continuous-mode
-    syndrome spread over `split` blocks per tile (8 rows per wave, 8 edge
-    parts per row), the last block per tile running the lane bookkeeping and
-    the variable launch writing the finished codewords' outputs."""
-    monkeypatch.setenv("LDPC_SYN_SPLIT", str(split))
-    monkeypatch.setenv("LDPC_SYN_FUSED", "0")
-    monkeypatch.setenv("LDPC_CONT", "1")
-    monkeypatch.setenv("LDPC_RES", "0")
-    monkeypatch.setenv("LDPC_RES_MSA_C", "0")
-    monkeypatch.setenv("LDPC_MSA_C", str(msa_c))
-    monkeypatch.setenv("LDPC_GROUP_TILES", str(group))
-    G2 = gpu.Graph(PCHK)
-    if algo == "bp":
-        llr = np.concatenate([synth.bsc_llrs(codewords, 0, 300, seed=3, p=0.003),
-                              synth.bsc_llrs(codewords, 300, 100, seed=2026, p=0.02)])
-        _, _, it, _ = _cmp(G2, og, llr, 30, chunk=chunk)
-    else:
-        llr = synth.bsc_llrs(codewords, 0, 400, seed=2026, p=0.002)
-        _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", chunk=chunk)
-    assert len(np.unique(it)) > 2
-    _cmp(G2, og, llr[:70], 0, algo=algo, chunk=chunk)
-    _cmp(G2, og, llr[:3], 20, algo=algo, chunk=chunk)
-
-
-@pytest.mark.parametrize("algo,msa_c,tiles,split", [("bp", 0, 3, 32), ("bp", 0, 1, 5), ("msa", 0, 2, 64), ("msa", 1, 2, 16)])
-def test_resident_pool_split_syndrome_bitexact(gpu, og, codewords, monkeypatch, algo, msa_c, tiles, split):
-    """LDPC_RES_SYN > 0: the resident pool with a separate multi-block
-    syndrome launch (k_syndrome_split) before a plain in-place check."""
-    monkeypatch.setenv("LDPC_RES", "1")
-    monkeypatch.setenv("LDPC_RES_MSA_C", "1")
-    monkeypatch.setenv("LDPC_RES_SYN", str(split))
-    monkeypatch.setenv("LDPC_RES_TILES", str(tiles))
-    monkeypatch.setenv("LDPC_RES_TILES_MSA_C", str(tiles))
-    monkeypatch.setenv("LDPC_MSA_C", str(msa_c))
-    monkeypatch.setenv("LDPC_CONT", "1")
-    G2 = gpu.Graph(PCHK)
-    if algo == "bp":
-        llr = np.concatenate([synth.bsc_llrs(codewords, 0, 200, seed=3, p=0.003),
-                              synth.bsc_llrs(codewords, 200, 100, seed=2026, p=0.02)])
-        _, _, it, _ = _cmp(G2, og, llr, 30, chunk=64 * tiles)
-    else:
-        llr = synth.bsc_llrs(codewords, 0, 300, seed=2026, p=0.002)
-        _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", chunk=64 * tiles)
-    assert len(np.unique(it)) > 2
-    _cmp(G2, og, llr[:70], 0, algo=algo, chunk=64 * tiles)
-    _cmp(G2, og, llr[:3], 20, algo=algo, chunk=64 * tiles)
-
-
-@pytest.mark.parametrize("algo,tiles,mode", [("bp", 3, 1), ("bp", 2, 2), ("bp", 1, 1), ("msa", 3, 2), ("bp", 3, 2), ("bp", 3, 3), ("msa", 2, 3)])
-def test_resident_pool_tile_streams_bitexact(gpu, og, codewords, monkeypatch, algo, tiles, mode):
-    """LDPC_RES_STREAMS: the resident pool with one HIP stream per pool tile
-    (independent check/variable chains, per-tile occupancy counters, a join
-    back into the engine stream at the end).  Pools of 1-3 tiles with refills,
-    mixed exits, max_iter 0 and batches smaller than the pool."""
-    monkeypatch.setenv("LDPC_RES", "1")
-    monkeypatch.setenv("LDPC_RES_STREAMS", str(mode))
-    monkeypatch.setenv("LDPC_MSA_C", "0")
-    monkeypatch.setenv("LDPC_CONT", "1")
-    G2 = gpu.Graph(PCHK)
-    if algo == "bp":
-        llr = np.concatenate([synth.bsc_llrs(codewords, 0, 200, seed=3, p=0.003),
-                              synth.bsc_llrs(codewords, 200, 100, seed=2026, p=0.02)])
-        _, _, it, _ = _cmp(G2, og, llr, 30, chunk=64 * tiles)
-        _cmp(G2, og, synth.dna_like_llrs(codewords, seed=1, reads=57000)[:150], 60, chunk=64 * tiles)
-    else:
-        llr = synth.bsc_llrs(codewords, 0, 300, seed=2026, p=0.002)
-        _, _, it, _ = _cmp(G2, og, llr, 50, algo="msa", chunk=64 * tiles)
-    assert len(np.unique(it)) > 2
-    _cmp(G2, og, llr[:70], 0, algo=algo, chunk=64 * tiles)
-    _cmp(G2, og, llr[:3], 20, algo=algo, chunk=64 * tiles)
-
-
-@pytest.mark.parametrize("tiles,cpw,poll", [(2, 4, 4), (3, 4, 1), (3, 2, 3), (4, 8, 2), (2, 8, 1)])
-def test_pingpong_bitexact(gpu, og, codewords, monkeypatch, tiles, cpw, poll):
-    """Ping-pong schedule of the resident BP pool (kernels.hpp k_pingpong_bp:
-    one launch = check(tile t) + variable(tile t-1)): only the launch grouping
-    across codewords changes, never a codeword's arithmetic -- mixed early
-    exits, all lanes at max_iter, max_iter 0, batches smaller than the pool,
-    posterior ratio, NaN / inf inputs."""
-    monkeypatch.setenv("LDPC_PINGPONG", "1")
-    monkeypatch.setenv("LDPC_RES", "1")
-    monkeypatch.setenv("LDPC_RES_TILES", str(tiles))
-    monkeypatch.setenv("LDPC_RES_POLL", str(poll))
-    monkeypatch.setenv("LDPC_PP_CPW", str(cpw))
-    G2 = gpu.Graph(PCHK)
-    e = gpu.Engine(G2, 0, "bp", chunk=64 * tiles)
-    assert e.pingpong and e.resident
-    del e
-    llr = synth.dna_like_llrs(codewords, seed=1, reads=57000)[:200]
-    _cmp(G2, og, llr, 60, chunk=64 * tiles)
-    llr = np.concatenate([synth.bsc_llrs(codewords, 0, 150, seed=3, p=0.003),
-                          synth.bsc_llrs(codewords, 150, 130, seed=2026, p=0.02)])
-    _, _, it, _ = _cmp(G2, og, llr, 50, chunk=64 * tiles)
-    assert (it[150:] == 50).all() and len(np.unique(it[:150])) > 2
-    _cmp(G2, og, llr[:70], 0, chunk=64 * tiles)
-    _cmp(G2, og, llr[:5], 50, chunk=64 * tiles)
-    _cmp(G2, og, llr[:130], 7, chunk=64 * tiles)
-    rng = np.random.default_rng(21)
-    llr = synth.dna_like_llrs(codewords, seed=2, reads=60000)[:100]
-    llr[rng.random(llr.shape) < 0.002] = np.nan
-    llr[rng.random(llr.shape) < 0.002] = np.inf
-    llr[rng.random(llr.shape) < 0.002] = -np.inf
-    ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 40, algo=0, post_mode=1, threads=8)
-    h, p, it, v = G2.decode(llr, max_iter=40, algo="bp", post="ratio", chunk=64 * tiles)
-    assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
-    nan = np.isnan(ref_p)
-    assert np.array_equal(np.isnan(p), nan)
-    assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64))
-
-
-def test_host_lr_table_path(G, og, codewords, monkeypatch):
+def test_host_lr_table_path(G, og, codewords):
     """ldpc_decode's LR table path (capi.cpp): LLRs that are exact multiples
     k * unit (the DNA alphabet) cross PCIe as one byte each and become
     table[k] = host exp(k * unit), the same bits as exp(LLR).  Bit-exact
-    against the oracle (host exp), identical to the exp path (LDPC_LR_TABLE=0),
+    against the oracle (host exp), identical to the exp path (lr_table off),
     and batches off the alphabet (several units, a non-multiple, NaN) fall
     back to the host exp."""
     llr = synth.dna_like_llrs(codewords, seed=5, reads=60000)[:150]
     h1, p1, it1, v1 = _cmp(G, og, llr, 60)
-    monkeypatch.setenv("LDPC_LR_TABLE", "0")
-    G0 = synth_graph = __import__("ldpc_amd").Graph(PCHK)
-    h0, p0, it0, v0 = G0.decode(llr, max_iter=60, post="ratio")
+    h0, p0, it0, v0 = G.decode(llr, max_iter=60, post="ratio", schedule=dict(lr_table=False))
     assert np.array_equal(h0, h1) and np.array_equal(it0, it1) and np.array_equal(p0.view(np.uint64), p1.view(np.uint64))
-    monkeypatch.delenv("LDPC_LR_TABLE")
     mixed = llr[:40].copy()
     mixed[7] *= 1.5  # a second unit
     mixed[9, 100] = 0.123  # off the alphabet
@@ -597,12 +427,12 @@ def test_host_lr_table_path(G, og, codewords, monkeypatch):
 
 
 
-def test_single_fill_first_check_from_prior(gpu, G, og, codewords, monkeypatch):
+def test_single_fill_first_check_from_prior(gpu, G, og, codewords):
     """A batch that fits the lane pool in one fill (the DNA batch through
     ldpc_decode): the refill stores only the prior and the first check takes
     d0 = 1 - 2/(1+LR) from it (k_check_bp_first) instead of E stored copies.
     Bit-exact against the oracle and identical to the stored-copies path
-    (LDPC_FIRST_FROM_PRIOR=0) at max_iter 0 / 1 / 2 / 60, with NaN / +-inf
+    (first_from_prior off) at max_iter 0 / 1 / 2 / 60, with NaN / +-inf
     inputs, for host LR (ldpc_decode) and device exp (Engine, LLR input)."""
     rng = np.random.default_rng(33)
     nasty = synth.dna_like_llrs(codewords, seed=6, reads=57000)[:150]
@@ -614,16 +444,14 @@ def test_single_fill_first_check_from_prior(gpu, G, og, codewords, monkeypatch):
     for llr, it in cases:
         ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, it, algo=0, post_mode=1, threads=8)
         outs = []
-        for fp in ("1", "0"):
-            monkeypatch.setenv("LDPC_FIRST_FROM_PRIOR", fp)
-            h, p, i, v = G.decode(llr, max_iter=it, post="ratio")
+        for fp in (True, False):
+            h, p, i, v = G.decode(llr, max_iter=it, post="ratio", schedule=dict(first_from_prior=fp))
             assert np.array_equal(i, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
             nan = np.isnan(ref_p)
             assert np.array_equal(np.isnan(p), nan)
             assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64))
             outs.append((h, i))
         assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
-    monkeypatch.delenv("LDPC_FIRST_FROM_PRIOR")
     # device-resident engine, LLR input (device exp in the refill), one fill of 150
     L = gpu
     llr = synth.dna_like_llrs(codewords, seed=8, reads=58000)[:150]

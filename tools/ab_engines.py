@@ -2,11 +2,12 @@
 workload (the bench's BSC config 3 input), alternating variants so clock,
 thermal and allocation effects hit both alike.
 
-    python tools/ab_engines.py --var A:LDPC_VAR_CPW=1 --var B:LDPC_VAR_CPW=8 --reps 6
+    python tools/ab_engines.py --var A:var_cpw=1 --var B:var_cpw=8 --reps 6
 
-Each variant is NAME:ENV=VAL[,ENV=VAL...]; the env is applied while that
-variant's engine is created (the engine reads it at init).  Prints one JSON
-line per variant with the median/min seconds per decode and cw/s.
+Each variant is NAME:KEY=VAL[,KEY=VAL...], KEY a ldpc_schedule keyword
+(ldpc_amd.Schedule.make: resident, group_tiles, var_cpw, ...) or `chunk`.
+Prints one JSON line per variant with the median/min seconds per decode and
+cw/s.
 """
 import argparse
 import json
@@ -44,19 +45,13 @@ def main():
     d_in = L.DeviceBuffer(0, B * N * 8)
     d_h, d_i, d_v = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
     def make(spec):
-        name, _, envs = spec.partition(":")
-        saved = {}
-        for kv in filter(None, envs.split(",")):
+        name, _, kvs = spec.partition(":")
+        kw = {}
+        for kv in filter(None, kvs.split(",")):
             k, v = kv.split("=", 1)
-            saved[k] = os.environ.get(k)
-            os.environ[k] = v
-        e = L.Engine(G, 0, args.algo, chunk=args.chunk)
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-        return name, e
+            kw[k] = int(v)
+        chunk = kw.pop("chunk", args.chunk)
+        return name, L.Engine(G, 0, args.algo, chunk=chunk, schedule=kw)
 
     if args.fresh:
         gen = None
@@ -94,18 +89,7 @@ def main():
 
     engines = []
     for spec in args.var:
-        name, _, envs = spec.partition(":")
-        saved = {}
-        for kv in filter(None, envs.split(",")):
-            k, v = kv.split("=", 1)
-            saved[k] = os.environ.get(k)
-            os.environ[k] = v
-        e = L.Engine(G, 0, args.algo, chunk=args.chunk)
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        name, e = make(spec)
         if args.profile:
             e.profile(args.profile)
         engines.append((name, e))
