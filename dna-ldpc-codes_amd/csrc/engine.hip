@@ -112,7 +112,7 @@ Engine::~Engine()
     for (auto e : ev_pool) hipEventDestroy(e);
     hipFree(d_fresh); hipFree(d_occ); hipFree(d_lane_b); hipFree(d_lane_n); hipFree(d_ctr);
     if (h_poll) hipHostFree(h_poll);
-    hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge); hipFree(d_col_row);
+    hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge); hipFree(d_col_er);
     hipFree(d_unsat); hipFree(d_done); hipFree(d_fin); hipFree(d_fin_b); hipFree(d_fin_n);
     hipFree(d_sgn);
     hipFree(v2c); if (c2v != v2c) hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
@@ -129,20 +129,16 @@ static int upload(T** dst, const std::vector<T>& v)
     return LDPC_OK;
 }
 
-// MSA-C scratch of `tiles` group tiles: records {min1, min2} [tiles][M][64],
-// meta words [tiles][M][64] u32, NaN planes [tiles][M][2][64] fp64
+// MSA-C scratch of `tiles` group tiles: record planes [tiles][M][4][64] fp64
+// (m1, m2, n0, n1), then the meta words [tiles][M][64] u32
 static size_t msa_scratch_bytes(int64_t tiles, int32_t M)
 {
-    return (size_t)tiles * M * dev::TILE * (sizeof(double2) + sizeof(uint32_t) + 2 * sizeof(double));
+    return (size_t)tiles * M * dev::TILE * (dev::MSA_REC_PLANES * sizeof(double) + sizeof(uint32_t));
 }
-static double2* msa_rec(double* scratch) { return reinterpret_cast<double2*>(scratch); }
+static double* msa_rec(double* scratch) { return scratch; }
 static uint32_t* msa_meta(double* scratch, int64_t tiles, int32_t M)
 {
-    return reinterpret_cast<uint32_t*>(msa_rec(scratch) + (size_t)tiles * M * dev::TILE);
-}
-static double* msa_nanp(double* scratch, int64_t tiles, int32_t M)
-{
-    return reinterpret_cast<double*>(msa_meta(scratch, tiles, M) + (size_t)tiles * M * dev::TILE);
+    return reinterpret_cast<uint32_t*>(scratch + (size_t)tiles * M * dev::MSA_REC_PLANES * dev::TILE);
 }
 
 int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, const ldpc_schedule* schedule)
@@ -202,10 +198,12 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     if ((rc = upload(&d_row_ptr, g->row_ptr)) || (rc = upload(&d_col_idx, g->col_idx)) ||
         (rc = upload(&d_col_ptr, g->col_ptr)) || (rc = upload(&d_col_edge, g->col_edge)))
         return rc;
-    if (msa_c) {
-        std::vector<int32_t> cr(g->col_edge.size());
-        for (size_t q = 0; q < cr.size(); q++) cr[q] = g->edge_row[(size_t)g->col_edge[q]];
-        if ((rc = upload(&d_col_row, cr))) return rc;
+    if (msa_c) {  // (row << 18) | edge id per CSC position (k_var_msa_c); E < 2^18 (above), M < 2^14
+        if (g->M >= (1 << (32 - dev::MSA_ER_SHIFT))) { set_error("MSA-C: too many rows"); return LDPC_ERR_UNSUPPORTED; }
+        std::vector<uint32_t> er(g->col_edge.size());
+        for (size_t q = 0; q < er.size(); q++)
+            er[q] = ((uint32_t)g->edge_row[(size_t)g->col_edge[q]] << dev::MSA_ER_SHIFT) | (uint32_t)g->col_edge[q];
+        if ((rc = upload(&d_col_er, er))) return rc;
     }
     if (g->regular_dc && g->dc_max > 0) {
         std::vector<int32_t> T((size_t)g->dc_max * g->M);
@@ -429,7 +427,7 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
     }
     if (msa_c) {
         LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72>), grid, blk, 0, s, v2c, msa_rec(scratch),
-                                      msa_meta(scratch, c2v_tiles, M), msa_nanp(scratch, c2v_tiles, M), active, M, E, t0));
+                                      msa_meta(scratch, c2v_tiles, M), active, M, E, t0));
         return LDPC_OK;
     }
     if (reg72) {
@@ -490,12 +488,11 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
     if (msa_c) {  // N % 16 == 0 (init)
         const int cpw = var_cpw >= 4 ? 4 : var_cpw;
         const unsigned nb = gt * (unsigned)(N / (4 * cpw));
-        const double2* rec = msa_rec(scratch);
+        const double* rec = msa_rec(scratch);
         const uint32_t* meta = msa_meta(scratch, c2v_tiles, M);
-        const double* nanp = msa_nanp(scratch, c2v_tiles, M);
 #define VAR_MSA_C(CONT, CPW)                                                                                    \
-    klaunch((k_var_msa_c<72, 8, CONT, CPW>), dim3(nb), dim3(256), 0, s, rec, meta, nanp, v2c, prior, hard, d_sgn, \
-            active, d_col_edge, d_col_row, pt, N, M, E, t0, (uint32_t)gt, rf)
+    klaunch((k_var_msa_c<72, 8, CONT, CPW>), dim3(nb), dim3(256), 0, s, rec, meta, v2c, prior, hard, d_sgn, \
+            active, d_col_er, pt, N, M, E, t0, (uint32_t)gt, rf)
         LAUNCH_ON(s, K_VAR, {
             if (cnt && cpw == 4) VAR_MSA_C(true, 4);
             else if (cnt && cpw == 2) VAR_MSA_C(true, 2);

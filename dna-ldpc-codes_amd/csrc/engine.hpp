@@ -82,7 +82,7 @@ struct Engine {
     int32_t* d_col_idx_T = nullptr;  // [dc][M] for regular rows (syndrome gathers)
     int32_t* d_col_ptr = nullptr;
     int32_t* d_col_edge = nullptr;
-    int32_t* d_col_row = nullptr;  // [E] row of edge col_edge[q] (MSA-C record lookups)
+    uint32_t* d_col_er = nullptr;  // [E] (row << 18) | edge id of CSC position q (MSA-C record lookups)
     // decoder state
     double* v2c = nullptr;
     double* c2v = nullptr;

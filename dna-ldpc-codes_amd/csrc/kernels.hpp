@@ -917,13 +917,11 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
 // graphs with E < 2^18).  A row's DC outgoing messages take only four
 // magnitudes -- min1, min2 and, in the NaN cases derived above k_check_msa,
 // |x_0| or |x_1| -- and a sign, so the check phase writes per (row, lane):
-//   rec  [group tile][M][64] {min1, min2}: 16 B per lane, one contiguous
-//        1-KB store per wave (and one 16-B load per lane and edge in the
-//        variable phase, independent of the meta word)
+//   rec  [group tile][M][4][64] fp64 planes m1, m2, n0 = |x_0|, n1 = |x_1|
+//        (n0 / n1 written only when NaN)
 //   meta [group tile][M][64] u32: bit 31 the row's sign parity, bit 30 NaN at
 //        x_1, bit 29 NaN at x_0, bits 0-17 the edge id of min1 (row * DC +
 //        i1; MSA_META_NONE: no minimum, every |x| inf or NaN)
-//   nanp [group tile][M][2][64] fp64 |x_0|, |x_1| -- written only when NaN
 // and nothing per edge.  The variable phase rebuilds each c2v from the meta
 // word, its own edge id and the sign bit of the v2c it stored itself (sgn,
 // !(x >= 0) of exactly that value -- the check's sign rule):
@@ -934,17 +932,22 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
 // included); a NaN's sign is never observed downstream (comparisons, fabs and
 // sums only), so every sum and decision is unchanged.  Per edge and codeword
 // the c2v stream shrinks from 16 B (fp64 write + read) to the records, which
-// the row's DC columns re-read from the XCD's L2 (see k_var_msa_c).
+// the row's DC columns re-read from the XCD's L2 (see k_var_msa_c).  Planes,
+// not {m1, m2} pairs: a wave needs m2 only in the lanes whose codeword has
+// its row minimum at this edge (1 in DC), so it fetches the m1 plane's 512 B
+// and only the m2 lines holding such a lane -- a pair layout fetches 1 KB per
+// edge, which measured 16 % slower (the variable kernel is bound by L2
+// requests; profiles/r3).
 // ---------------------------------------------------------------------------
+constexpr int MSA_REC_PLANES = 4;
 constexpr uint32_t MSA_META_NONE = 0x3ffffu;  // meta: no min1 (edge ids must stay below it)
 
 // grid (ceil(M/4), group tiles), block 256: one wave per (row, tile); the
 // v2c group is streamed once, nontemporal.
 template <int DC>
-__global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, double2* __restrict__ rec,
-                                                     uint32_t* __restrict__ meta, double* __restrict__ nanp,
-                                                     const uint64_t* __restrict__ active, int32_t M, int64_t E,
-                                                     int64_t t0)
+__global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, double* __restrict__ rec,
+                                                     uint32_t* __restrict__ meta, const uint64_t* __restrict__ active,
+                                                     int32_t M, int64_t E, int64_t t0)
 {
     static_assert(DC >= 2 && DC <= 96, "row degree");
     const int lane = lane_id();
@@ -979,13 +982,14 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     neg &= 1u;
     const double a0 = __builtin_fabs(x[0]), a1 = __builtin_fabs(x[1]);
     const bool nan0 = __builtin_isnan(a0), nan1 = __builtin_isnan(a1);
-    const size_t ri = ((size_t)blockIdx.y * M + row) * TILE + lane;
-    rec[ri] = make_double2(m1, m2);
-    meta[ri] = (neg << 31) | ((nan1 ? 1u : 0u) << 30) | ((nan0 ? 1u : 0u) << 29) |
-               (i1 < 0 ? MSA_META_NONE : (uint32_t)(row * DC + i1));
-    double* __restrict__ np = nanp + ((size_t)blockIdx.y * M + row) * (2 * TILE) + lane;
-    if (nan0) np[0] = a0;
-    if (nan1) np[TILE] = a1;
+    double* __restrict__ r = rec + ((size_t)blockIdx.y * M + row) * (MSA_REC_PLANES * TILE) + lane;
+    r[0] = m1;
+    r[TILE] = m2;
+    if (nan0) r[2 * TILE] = a0;
+    if (nan1) r[3 * TILE] = a1;
+    meta[((size_t)blockIdx.y * M + row) * TILE + lane] =
+        (neg << 31) | ((nan1 ? 1u : 0u) << 30) | ((nan0 ? 1u : 0u) << 29) |
+        (i1 < 0 ? MSA_META_NONE : (uint32_t)(row * DC + i1));
 }
 
 __device__ __forceinline__ double flip_sign(double v, uint32_t neg)
@@ -993,21 +997,39 @@ __device__ __forceinline__ double flip_sign(double v, uint32_t neg)
     return __longlong_as_double(__double_as_longlong(v) ^ ((long long)(neg & 1u) << 63));
 }
 
+// Raw buffer resource over [base, base + bytes) (gfx9 data format, no
+// swizzle, stride 0).  A wave's gathers and scatters then take a
+// wave-uniform byte offset in an SGPR (soffset) and one shared per-lane
+// offset in a VGPR: no per-edge 64-bit address arithmetic on the VALU.
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kBufNT = 2;  // cache-policy bits of a buffer access: nt (gfx950), as __builtin_nontemporal_store
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint64_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                            (int)(bytes < 0x7fffffffull ? bytes : 0x7fffffffull), 0x00020000);
+}
+
+// MSA-C column table: per CSC position q (column j's edges, ascending row),
+// (row of edge << 18) | edge id -- one wave-uniform word per edge (E < 2^18,
+// M < 2^14), so a wave's CPW x DV edges take CPW x DV SGPRs
+constexpr int MSA_ER_SHIFT = 18;
+
 // Min-sum variable phase on compressed messages (the arithmetic of k_var_m<MSA>).
 // 1-D grid of gt * (N / (4 CPW)) blocks; block L works on group tile L % gt.
 // Workgroups are dispatched to the 8 XCDs round-robin, so when gt divides 8
 // every XCD only ever touches the records of one tile (2.5 MB for the DNA
 // code), which stay in its 4 MB L2 while the tile's DC columns per row re-read
 // them.  Every record and meta load of the wave's CPW columns is issued before
-// the first use (no load depends on another), and the v2c stores are
-// nontemporal (the group's v2c is read back once, by the next check phase).
+// the first use (no load depends on another), all through buffer resources
+// (per-edge offsets in SGPRs), and the v2c stores are nontemporal (the
+// group's v2c is read back once, by the next check phase).
 template <int DC, int DV, bool CONT, int CPW>
-__global__ __launch_bounds__(256) void k_var_msa_c(const double2* __restrict__ rec, const uint32_t* __restrict__ meta,
-                                                   const double* __restrict__ nanp, double* __restrict__ v2c,
+__global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ rec, const uint32_t* __restrict__ meta,
+                                                   double* __restrict__ v2c,
                                                    double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                    uint8_t* __restrict__ sgn, const uint64_t* __restrict__ active,
-                                                   const int32_t* __restrict__ col_edge,
-                                                   const int32_t* __restrict__ col_row, double* __restrict__ post,
+                                                   const uint32_t* __restrict__ col_er, double* __restrict__ post,
                                                    int32_t N, int32_t M, int64_t E, int64_t t0, uint32_t gt, Refill rf)
 {
     const int lane = lane_id();
@@ -1031,18 +1053,14 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double2* __restrict__ r
         fb = rf.fin_b[t * TILE + lane];
         fn = rf.fin_n[t * TILE + lane];
     }
-    const size_t tb = (size_t)t * E;
-    int32_t eid[CPW][DV], rid[CPW][DV];
+    uint32_t er[CPW][DV];
 #pragma unroll
     for (int c = 0; c < CPW; ++c)
 #pragma unroll
-        for (int s = 0; s < DV; ++s) {
-            eid[c][s] = col_edge[(size_t)(j0 + c) * DV + s];
-            rid[c][s] = col_row[(size_t)(j0 + c) * DV + s];
-        }
-    // wave-uniform bases: per-edge addresses are a scalar base + the lane offset
-    const double2* __restrict__ rg = rec + (size_t)ty * M * TILE;
-    const uint32_t* __restrict__ mg = meta + (size_t)ty * M * TILE;
+        for (int s = 0; s < DV; ++s) er[c][s] = col_er[(size_t)(j0 + c) * DV + s];
+    const auto rrec = buf_rsrc(rec + (size_t)ty * M * (MSA_REC_PLANES * TILE), (uint64_t)M * MSA_REC_PLANES * TILE * 8);
+    const auto rmeta = buf_rsrc(meta + (size_t)ty * M * TILE, (uint64_t)M * TILE * sizeof(uint32_t));
+    const auto rv2c = buf_rsrc(v2c + (size_t)t * E * TILE, (uint64_t)E * TILE * sizeof(double));
     double l[CPW][DV], pv[CPW], xin[CPW];
     if (fr) {
         const double* __restrict__ in_row = rf.in + (size_t)rf.lane_b[t * TILE + lane] * N;
@@ -1050,16 +1068,22 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double2* __restrict__ r
         for (int c = 0; c < CPW; ++c) xin[c] = in_row[j0 + c];
     }
     if (live) {
+        // the meta words and the m1 plane first (independent loads), then the
+        // m2 plane only in the lanes that need it (an exec-masked load: the
+        // other lanes' lines are not fetched)
+        constexpr int PB = TILE * 8;  // bytes per record plane of one row
         uint32_t sb[CPW], mw[CPW][DV];
-        double2 rr[CPW][DV];
+        double r1[CPW][DV];
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             pv[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
             sb[c] = sgn[((size_t)t * N + j0 + c) * TILE + lane];
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
-                mw[c][s] = (mg + (size_t)rid[c][s] * TILE)[lane];
-                rr[c][s] = (rg + (size_t)rid[c][s] * TILE)[lane];
+                const int rid = (int)(er[c][s] >> MSA_ER_SHIFT);
+                mw[c][s] = __builtin_amdgcn_raw_buffer_load_b32(rmeta, lane * 4, rid * (TILE * 4), 0);
+                r1[c][s] = __builtin_bit_cast(
+                    double, __builtin_amdgcn_raw_buffer_load_b64(rrec, lane * 8, rid * (MSA_REC_PLANES * PB), 0));
             }
         }
         uint32_t anynan = 0;
@@ -1069,7 +1093,13 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double2* __restrict__ r
             for (int s = 0; s < DV; ++s) {
                 const uint32_t m = mw[c][s];
                 anynan |= m;
-                const double mag = ((m & MSA_META_NONE) == (uint32_t)eid[c][s]) ? rr[c][s].y : rr[c][s].x;
+                const bool is1 = (m & MSA_META_NONE) == (er[c][s] & MSA_META_NONE);
+                double mag = r1[c][s];
+                if (is1) {
+                    const int rid = (int)(er[c][s] >> MSA_ER_SHIFT);
+                    mag = __builtin_bit_cast(
+                        double, __builtin_amdgcn_raw_buffer_load_b64(rrec, lane * 8, rid * (MSA_REC_PLANES * PB) + PB, 0));
+                }
                 l[c][s] = flip_sign(mag, (m >> 31) ^ (sb[c] >> s));
             }
         if (__builtin_expect(__ballot((anynan >> 29) & 3u) != 0ull, 0)) {
@@ -1079,9 +1109,10 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double2* __restrict__ r
 #pragma unroll
                 for (int s = 0; s < DV; ++s) {
                     const uint32_t m = mw[c][s];
-                    const bool first = eid[c][s] % DC == 0;  // edges are numbered row-major
+                    const uint32_t eid = er[c][s] & MSA_META_NONE, rid = er[c][s] >> MSA_ER_SHIFT;
+                    const bool first = eid % DC == 0;  // edges are numbered row-major
                     if ((m >> (first ? 30 : 29)) & 1u) {
-                        const double nv = nanp[((size_t)ty * M + rid[c][s]) * (2 * TILE) + (first ? TILE : 0) + lane];
+                        const double nv = rec[(((size_t)ty * M + rid) * MSA_REC_PLANES + (first ? 3 : 2)) * TILE + lane];
                         l[c][s] = flip_sign(nv, (m >> 31) ^ (sb[c] >> s));
                     }
                 }
@@ -1128,11 +1159,14 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double2* __restrict__ r
         }
         if (CONT && fr) prior[pj] = xin[c];
         if (line_occupied(touched, lane) || fr || live) {  // whole-line stores, as k_var_m
-#pragma unroll
-            for (int s = 0; s < DV; ++s) st<true>(v2c + (tb + eid[c][s]) * TILE + lane, dv[s]);
             uint32_t sbn = 0;
 #pragma unroll
-            for (int s = 0; s < DV; ++s) sbn |= (dv[s] >= 0 ? 0u : 1u) << s;
+            for (int s = 0; s < DV; ++s) {
+                const int eid = (int)(er[c][s] & MSA_META_NONE);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, dv[s]), rv2c, lane * 8,
+                                                      eid * (TILE * 8), kBufNT);
+                sbn |= (dv[s] >= 0 ? 0u : 1u) << s;
+            }
             sgn[pj] = (uint8_t)sbn;
         }
         const uint64_t m = __ballot(h);

@@ -57,6 +57,10 @@ def test_two_rank_bench_shards_match_single_process(gpu, G, tmp_path):
     out2 = _line(r.stdout)
     assert out2["n_gpus"] == 2 and out2["scaling"] == "strong"
     assert out2["config"]["per_rank"] == [500, 500] and out2["config"]["global_batch"] == total
+    # every rank checked a sample of its own shard against the oracle
+    ck = out2["check"]
+    assert ck["mismatches"] == 0 and [p["rank"] for p in ck["per_rank"]] == [0, 1]
+    assert [p["b0"] for p in ck["per_rank"]] == [0, 500] and all(p["checked"] >= 16 for p in ck["per_rank"])
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dump-dir", d1, *args], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-3000:]
