@@ -159,7 +159,9 @@ def kernel_names(eng, algo) -> dict:
     them (tools/pmc_r3.py short form)."""
     msa = "true" if algo == "msa" else "false"
     if eng.msa_compressed:
-        return {"check": "k_check_msa_c<72>", "variable": f"k_var_msa_c<72,8,{str(eng.continuous).lower()},4>"}
+        nt = str(eng.nontemporal).lower()
+        return {"check": f"k_check_msa_c<72,{nt}>",
+                "variable": f"k_var_msa_c<72,8,{str(eng.continuous).lower()},{VAR_CPW},{nt}>"}
     chk = "k_check_msa" if algo == "msa" else "k_check_bp"
     if eng.resident:
         return {"check": f"{chk}<72,false,true>", "variable": f"k_var_m<{msa},8,false,true,{VAR_CPW},true>"}

@@ -606,9 +606,12 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
             }
             E.tie_base = c0(c);  // tie hash keyed by the codeword's index in this call
             LDPC_HIP(hipStreamWaitEvent(E.stream, S.ev_h2d[k], 0));
+            const double td0 = api_timing ? now() : 0;
             int r = E.decode(S.d_in[k], in_kind, Bc, max_iter, S.d_hard[k], post_out ? S.d_post[k] : nullptr,
                              o.post_kind, S.d_iters[k], S.d_valid[k]);
             if (r) return r;
+            if (api_timing)
+                std::fprintf(stderr, "api chunk %lld: decode enqueue + drain wait %.3f ms\n", (long long)c, now() - td0);
             LDPC_HIP(hipEventRecord(S.ev_dec[k], E.stream));
             LDPC_HIP(hipStreamWaitEvent(S.copy_out, S.ev_dec[k], 0));
             if (S.d_hbits[k]) {  // 1/8 of the bytes across PCIe
@@ -629,6 +632,7 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
             LDPC_HIP(hipEventRecord(S.ev_d2h[k], S.copy_out));
             return LDPC_OK;
         };
+        const double t_call = api_timing ? now() : 0;
         rc = prep(0);
         for (int64_t c = 0; c < nch && rc == LDPC_OK; c++) {
             // the next chunk's host work and H2D run on a helper thread while
@@ -647,6 +651,7 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
             if (rc == LDPC_OK && rc_next) { rc = rc_next; set_error(err_next); }
         }
         if (rc == LDPC_OK) rc = finish(nch - 1);
+        if (api_timing) std::fprintf(stderr, "api shard %zu: %.3f ms\n", di, now() - t_call);
         if (rc == LDPC_OK && hipStreamSynchronize(E.stream) != hipSuccess) {  // surplus steps of the last decode
             set_error("hipStreamSynchronize failed");
             rc = LDPC_ERR_DEVICE;

@@ -53,16 +53,22 @@ constexpr int32_t kDefaultFlags = LDPC_SCHED_NONTEMPORAL | LDPC_SCHED_CONTINUOUS
                                   LDPC_SCHED_RESIDENT | LDPC_SCHED_FIRST_FROM_PRIOR | LDPC_SCHED_LR_TABLE;
 constexpr int32_t kAllFlags = kDefaultFlags | LDPC_SCHED_DEBUG_NO_DRAIN;
 
+// flags_set bits of a resolved schedule (never set by callers): resolved,
+// and whether the caller chose the resident pool (the auto-disable rule for
+// large explicit pools applies only when it did not)
+constexpr int32_t kResolved = 1 << 30, kResChosen = 1 << 29;
+
 ldpc_schedule resolve_schedule(const ldpc_schedule* s)
 {
+    if (s && (s->flags_set & kResolved)) return *s;  // idempotent
     ldpc_schedule r{};
     if (s) r = *s;
     r.flags = (kDefaultFlags & ~r.flags_set) | (r.flags & r.flags_set);
     r.flags &= kAllFlags;
-    // remember whether the caller chose the resident pool (auto-disable rule)
-    r.flags_set = kAllFlags | (s && (s->flags_set & LDPC_SCHED_RESIDENT) ? (1 << 30) : 0);
+    r.flags_set = kAllFlags | kResolved | ((r.flags_set & LDPC_SCHED_RESIDENT) ? kResChosen : 0);
     if (r.group_tiles == 0) r.group_tiles = -2;  // per-algorithm default, resolved at init
-    if (r.var_cpw != 1 && r.var_cpw != 2 && r.var_cpw != 4 && r.var_cpw != 8) r.var_cpw = kDefaultVarCpw;
+    // (3: compressed min-sum only; the fp64 variable kernels take 1, 2, 4 or 8)
+    if (r.var_cpw < 1 || r.var_cpw > 8 || (r.var_cpw > 4 && r.var_cpw != 8)) r.var_cpw = kDefaultVarCpw;
     if (r.pool_tiles <= 0) r.pool_tiles = kDefaultPoolTiles;
     if (r.poll_every <= 0) r.poll_every = kDefaultResPoll;
     if (r.syn_blocks <= 0) r.syn_blocks = kDefaultSynBlocks;
@@ -168,7 +174,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     // by default the resident pool is the Infinity-Cache-sized one: a caller's
     // explicit larger pool (the host API's chunks, the DNA batch) runs the
     // grouped schedule (A/B, 272-codeword DNA batch at cap 320: 193k -> 250k cw/s)
-    const bool res_chosen = (sched.flags_set & (1 << 30)) != 0;
+    const bool res_chosen = (sched.flags_set & kResChosen) != 0;
     if (res && !res_chosen && chunk > kResAutoMaxTiles * 64) res = false;
     nt_d = sched_flag(sched, LDPC_SCHED_NONTEMPORAL) && !res;  // the pool is meant to stay cached
     debug_no_drain = sched_flag(sched, LDPC_SCHED_DEBUG_NO_DRAIN);
@@ -426,8 +432,12 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
         return LDPC_OK;
     }
     if (msa_c) {
-        LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72>), grid, blk, 0, s, v2c, msa_rec(scratch),
-                                      msa_meta(scratch, c2v_tiles, M), active, M, E, t0));
+        if (nt_d)
+            LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, true>), grid, blk, 0, s, v2c, msa_rec(scratch),
+                                          msa_meta(scratch, c2v_tiles, M), active, M, E, t0));
+        else
+            LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, false>), grid, blk, 0, s, v2c, msa_rec(scratch),
+                                          msa_meta(scratch, c2v_tiles, M), active, M, E, t0));
         return LDPC_OK;
     }
     if (reg72) {
@@ -486,27 +496,36 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
     const bool reg8 = g->regular_dv && g->dv_max == 8;
     const bool cnt = rf.fresh != nullptr;
     if (msa_c) {  // N % 16 == 0 (init)
-        const int cpw = var_cpw >= 4 ? 4 : var_cpw;
+        int cpw = var_cpw >= 4 ? 4 : var_cpw;
+        if (N % (4 * cpw) != 0) cpw = 1;  // (N % 16 == 0: every CPW but 3 divides)
         const unsigned nb = gt * (unsigned)(N / (4 * cpw));
         const double* rec = msa_rec(scratch);
         const uint32_t* meta = msa_meta(scratch, c2v_tiles, M);
-#define VAR_MSA_C(CONT, CPW)                                                                                    \
-    klaunch((k_var_msa_c<72, 8, CONT, CPW>), dim3(nb), dim3(256), 0, s, rec, meta, v2c, prior, hard, d_sgn, \
+#define VAR_MSA_C2(CONT, CPW, NT)                                                                                \
+    klaunch((k_var_msa_c<72, 8, CONT, CPW, NT>), dim3(nb), dim3(256), 0, s, rec, meta, v2c, prior, hard, d_sgn, \
             active, d_col_er, pt, N, M, E, t0, (uint32_t)gt, rf)
+#define VAR_MSA_C(CONT, CPW)              \
+    do {                                  \
+        if (nt_d) VAR_MSA_C2(CONT, CPW, true); \
+        else VAR_MSA_C2(CONT, CPW, false);     \
+    } while (0)
         LAUNCH_ON(s, K_VAR, {
             if (cnt && cpw == 4) VAR_MSA_C(true, 4);
+            else if (cnt && cpw == 3) VAR_MSA_C(true, 3);
             else if (cnt && cpw == 2) VAR_MSA_C(true, 2);
             else if (cnt) VAR_MSA_C(true, 1);
             else if (cpw == 4) VAR_MSA_C(false, 4);
+            else if (cpw == 3) VAR_MSA_C(false, 3);
             else if (cpw == 2) VAR_MSA_C(false, 2);
             else VAR_MSA_C(false, 1);
         });
 #undef VAR_MSA_C
+#undef VAR_MSA_C2
         return LDPC_OK;
     }
     if (reg8) {
         const bool inplace = scratch == v2c;
-        const int cpw = N % (4 * var_cpw) == 0 ? var_cpw : 1;
+        const int cpw = (var_cpw != 3 && N % (4 * var_cpw) == 0) ? var_cpw : 1;
         const dim3 grid((unsigned)((N + 4 * cpw - 1) / (4 * cpw)), gt);
         LAUNCH_ON(s, K_VAR, {
             if (algo == LDPC_ALGO_MSA) var_m<true>(nt_d, cnt, inplace, cpw, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf);

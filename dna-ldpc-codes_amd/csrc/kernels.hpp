@@ -105,7 +105,7 @@ __device__ __forceinline__ void store_fin_hard(const Refill& rf, const uint64_t*
 #pragma unroll
     for (int c = 0; c < CPW; ++c) v |= ((hw[c] >> lane) & 1ull) << (8 * c);
     uint8_t* p = rf.hard_out + (size_t)fb * N + j0;
-    if (rf.hard_vec) {
+    if (rf.hard_vec && (CPW == 8 || CPW == 4 || CPW == 2 || CPW == 1)) {
         if constexpr (CPW == 8) *reinterpret_cast<uint64_t*>(p) = v;
         else if constexpr (CPW == 4) *reinterpret_cast<uint32_t*>(p) = (uint32_t)v;
         else if constexpr (CPW == 2) *reinterpret_cast<uint16_t*>(p) = (uint16_t)v;
@@ -943,8 +943,8 @@ constexpr int MSA_REC_PLANES = 4;
 constexpr uint32_t MSA_META_NONE = 0x3ffffu;  // meta: no min1 (edge ids must stay below it)
 
 // grid (ceil(M/4), group tiles), block 256: one wave per (row, tile); the
-// v2c group is streamed once, nontemporal.
-template <int DC>
+// v2c group is streamed once (NT: nontemporal loads).
+template <int DC, bool NT>
 __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, double* __restrict__ rec,
                                                      uint32_t* __restrict__ meta, const uint64_t* __restrict__ active,
                                                      int32_t M, int64_t E, int64_t t0)
@@ -959,7 +959,7 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     const double* __restrict__ src = v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
     double x[DC];
 #pragma unroll
-    for (int k = 0; k < DC; ++k) x[k] = ld<true>(src + (size_t)k * TILE);
+    for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
     // one pass: min1 with its FIRST index, min2 = minimum over the other
     // indices (a tie with min1 gives min2 == min1), NaN never compares less
     double m1 = __builtin_inf(), m2 = __builtin_inf();
@@ -1022,9 +1022,9 @@ constexpr int MSA_ER_SHIFT = 18;
 // code), which stay in its 4 MB L2 while the tile's DC columns per row re-read
 // them.  Every record and meta load of the wave's CPW columns is issued before
 // the first use (no load depends on another), all through buffer resources
-// (per-edge offsets in SGPRs), and the v2c stores are nontemporal (the
-// group's v2c is read back once, by the next check phase).
-template <int DC, int DV, bool CONT, int CPW>
+// (per-edge offsets in SGPRs); NT: nontemporal v2c stores (the group's v2c is
+// read back once, by the next check phase).
+template <int DC, int DV, bool CONT, int CPW, bool NT>
 __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ rec, const uint32_t* __restrict__ meta,
                                                    double* __restrict__ v2c,
                                                    double* __restrict__ prior, uint64_t* __restrict__ hard,
@@ -1164,7 +1164,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             for (int s = 0; s < DV; ++s) {
                 const int eid = (int)(er[c][s] & MSA_META_NONE);
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, dv[s]), rv2c, lane * 8,
-                                                      eid * (TILE * 8), kBufNT);
+                                                      eid * (TILE * 8), NT ? kBufNT : 0);
                 sbn |= (dv[s] >= 0 ? 0u : 1u) << s;
             }
             sgn[pj] = (uint8_t)sbn;

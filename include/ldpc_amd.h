@@ -78,7 +78,8 @@ typedef struct ldpc_graph ldpc_graph;
  * measurements on MI355X.  The library reads no environment variable to pick
  * a schedule. */
 enum {
-    LDPC_SCHED_NONTEMPORAL = 1 << 0,    /* grouped schedule: nontemporal variable->check stream (default on) */
+    LDPC_SCHED_NONTEMPORAL = 1 << 0,    /* grouped schedule (and compressed min-sum): nontemporal
+                                           variable->check stream (default on) */
     LDPC_SCHED_CONTINUOUS = 1 << 3,     /* continuous batching: a finished codeword's lane is refilled with
                                            the next one (fp64 decoders on (8,72)-regular graphs; default on;
                                            needs hard / iters / valid outputs) */

@@ -5,6 +5,10 @@ template instantiation.
 
     python tools/pmc_r3.py <dir with pmc_*/run_counter_collection.csv> <bench .out> [out.json]
 
+To feed bench.py's roofline.traffic, merge the "per_cw_iter_by_instantiation"
+maps of the BP and min-sum summaries into profiles/r<N>/pmc_traffic.json
+(tools/pmc_r3.py --merge out.json a.json b.json ...).
+
 <bench .out> is the stdout of one of the passes (the bench JSON line): its
 config gives the executed codeword-iterations (batch x mean_iters x steps).
 Bytes: TCC_EA0_RDREQ x 128 + TCC_EA0_WRREQ x 64, the calibration of
@@ -37,7 +41,20 @@ def load(d):
     return agg
 
 
+def merge(out, parts):
+    m = {"what": "L2 -> fabric (EA) bytes per executed codeword-iteration of each decode kernel instantiation "
+                 "(TCC_EA0_RDREQ x 128 + TCC_EA0_WRREQ x 64; calibration profiles/r2/pmc_calib_and_decode.json)",
+         "sources": parts, "per_cw_iter_by_instantiation": {}}
+    for p in parts:
+        j = json.load(open(p))
+        m["per_cw_iter_by_instantiation"].update(j["per_cw_iter_by_instantiation"])
+    open(out, "w").write(json.dumps(m, indent=1) + "\n")
+    print(json.dumps(m, indent=1))
+
+
 def main():
+    if sys.argv[1] == "--merge":
+        return merge(sys.argv[2], sys.argv[3:])
     d, bench_out = sys.argv[1], sys.argv[2]
     line = [ln for ln in open(bench_out) if ln.startswith("{")][-1]
     bj = json.loads(line)
@@ -70,6 +87,9 @@ def main():
                 if q in cs:
                     e[q + "_per_wave"] = round(cs[q][0] / max(w, 1), 1)
         out["kernels"][k] = e
+    # bench.py's roofline.traffic lookup: EA bytes per executed codeword-iteration by instantiation
+    out["per_cw_iter_by_instantiation"] = {k: e["ea_bytes_per_cw_iter"] for k, e in out["kernels"].items()
+                                           if "ea_bytes_per_cw_iter" in e}
     js = json.dumps(out, indent=1)
     if len(sys.argv) > 3:
         open(sys.argv[3], "w").write(js + "\n")
