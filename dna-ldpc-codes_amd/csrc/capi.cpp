@@ -26,6 +26,7 @@
 #include "../../include/ldpc_amd.h"
 #include "engine.hpp"
 #include "graph.hpp"
+#include "host_simd.hpp"
 
 using ldpc::Engine;
 using ldpc::HostGraph;
@@ -125,20 +126,10 @@ double llr_unit(const double* src, int64_t rows, size_t N)
     return u;
 }
 
-// codes of LLRs [i0, i1); false when one is not k * unit with |k| <=
-// kCodeMax.  Branch-free (round to nearest by the 1.5 * 2^52 trick, |q| <
-// 2^51 here), so the compiler vectorises it.
+// codes of LLRs [i0, i1) (host_simd.cpp)
 bool encode_rows(const double* __restrict__ src, int8_t* __restrict__ code, size_t i0, size_t i1, double unit)
 {
-    const double inv = 1.0 / unit, magic = 6755399441055744.0, lim = kCodeMax;
-    int bad = 0;
-    for (size_t i = i0; i < i1; i++) {
-        const double x = src[i];
-        const double kd = (x * inv + magic) - magic;
-        bad |= (int)(kd * unit != x) | (int)!(kd <= lim && kd >= -lim);
-        code[i] = (int8_t)(int)std::fmin(std::fmax(kd, -lim), lim);
-    }
-    return bad == 0;
+    return ldpc::host_encode_lattice(src, code, i0, i1, unit, kCodeMax);
 }
 
 // byte x -> 8 bytes, byte r = bit r of x (unpacking the device's packed hard bits)

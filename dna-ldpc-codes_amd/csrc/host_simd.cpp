@@ -1,0 +1,29 @@
+// host_simd.cpp -- host-side vector loops of the C ABI, built by the host
+// compiler (not hipcc) so that target_clones can pick an AVX2 version at run
+// time where the host has it; the default clone is the baseline x86-64 one.
+// Both clones execute the same IEEE operations in the same order per
+// element, so they produce the same codes.
+#include "host_simd.hpp"
+
+#include <cmath>
+
+namespace ldpc {
+
+// Branch-free (round to nearest by the 1.5 * 2^52 trick, |q| < 2^51 here), so
+// the compiler vectorises it.
+__attribute__((target_clones("avx2", "default"))) bool host_encode_lattice(const double* __restrict__ src,
+                                                                             int8_t* __restrict__ code, size_t i0,
+                                                                             size_t i1, double unit, int kmax)
+{
+    const double inv = 1.0 / unit, magic = 6755399441055744.0, lim = kmax;
+    int bad = 0;
+    for (size_t i = i0; i < i1; i++) {
+        const double x = src[i];
+        const double kd = (x * inv + magic) - magic;
+        bad |= (int)(kd * unit != x) | (int)!(kd <= lim && kd >= -lim);
+        code[i] = (int8_t)(int)std::fmin(std::fmax(kd, -lim), lim);
+    }
+    return bad == 0;
+}
+
+}  // namespace ldpc

@@ -934,10 +934,10 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
 // the c2v stream shrinks from 16 B (fp64 write + read) to the records, which
 // the row's DC columns re-read from the XCD's L2 (see k_var_msa_c).  Planes,
 // not {m1, m2} pairs: a wave needs m2 only in the lanes whose codeword has
-// its row minimum at this edge (1 in DC), so it fetches the m1 plane's 512 B
-// and only the m2 lines holding such a lane -- a pair layout fetches 1 KB per
-// edge, which measured 16 % slower (the variable kernel is bound by L2
-// requests; profiles/r3).
+// its row minimum at this edge (1 in DC), so one load per edge from the plane
+// each lane needs fetches the m1 plane's 512 B and only the m2 lines holding
+// such a lane -- a pair layout fetches 1 KB per edge, which measured 16 %
+// slower (profiles/r3).
 // ---------------------------------------------------------------------------
 constexpr int MSA_REC_PLANES = 4;
 constexpr uint32_t MSA_META_NONE = 0x3ffffu;  // meta: no min1 (edge ids must stay below it)
@@ -1020,10 +1020,10 @@ constexpr int MSA_ER_SHIFT = 18;
 // Workgroups are dispatched to the 8 XCDs round-robin, so when gt divides 8
 // every XCD only ever touches the records of one tile (2.5 MB for the DNA
 // code), which stay in its 4 MB L2 while the tile's DC columns per row re-read
-// them.  Every record and meta load of the wave's CPW columns is issued before
-// the first use (no load depends on another), all through buffer resources
-// (per-edge offsets in SGPRs); NT: nontemporal v2c stores (the group's v2c is
-// read back once, by the next check phase).
+// them.  The meta loads of the wave's CPW columns go out together, then the
+// record loads (their plane depends on the meta word), all through buffer
+// resources (per-edge offsets in SGPRs); NT: nontemporal v2c stores (the
+// group's v2c is read back once, by the next check phase).
 template <int DC, int DV, bool CONT, int CPW, bool NT>
 __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ rec, const uint32_t* __restrict__ meta,
                                                    double* __restrict__ v2c,
@@ -1068,12 +1068,14 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
         for (int c = 0; c < CPW; ++c) xin[c] = in_row[j0 + c];
     }
     if (live) {
-        // the meta words and the m1 plane first (independent loads), then the
-        // m2 plane only in the lanes that need it (an exec-masked load: the
-        // other lanes' lines are not fetched)
+        // the meta words first; from them, per edge a 4-bit code (bit 0: the
+        // c2v sign = parity ^ own sign, bits 1-2: the record plane -- m2 at the
+        // row's min1 edge, a NaN plane when x_0 / x_1 is NaN, else m1), packed
+        // 8 to a register; then one record load per edge from the plane each
+        // lane needs: the wave fetches the m1 plane's lines plus only the m2
+        // lines holding a lane that needs them
         constexpr int PB = TILE * 8;  // bytes per record plane of one row
-        uint32_t sb[CPW], mw[CPW][DV];
-        double r1[CPW][DV];
+        uint32_t sb[CPW], mw[CPW][DV], cpk[CPW];
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             pv[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
@@ -1082,41 +1084,45 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             for (int s = 0; s < DV; ++s) {
                 const int rid = (int)(er[c][s] >> MSA_ER_SHIFT);
                 mw[c][s] = __builtin_amdgcn_raw_buffer_load_b32(rmeta, lane * 4, rid * (TILE * 4), 0);
-                r1[c][s] = __builtin_bit_cast(
-                    double, __builtin_amdgcn_raw_buffer_load_b64(rrec, lane * 8, rid * (MSA_REC_PLANES * PB), 0));
             }
         }
         uint32_t anynan = 0;
 #pragma unroll
-        for (int c = 0; c < CPW; ++c)
+        for (int c = 0; c < CPW; ++c) {
+            cpk[c] = 0;
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
                 const uint32_t m = mw[c][s];
                 anynan |= m;
-                const bool is1 = (m & MSA_META_NONE) == (er[c][s] & MSA_META_NONE);
-                double mag = r1[c][s];
-                if (is1) {
-                    const int rid = (int)(er[c][s] >> MSA_ER_SHIFT);
-                    mag = __builtin_bit_cast(
-                        double, __builtin_amdgcn_raw_buffer_load_b64(rrec, lane * 8, rid * (MSA_REC_PLANES * PB) + PB, 0));
-                }
-                l[c][s] = flip_sign(mag, (m >> 31) ^ (sb[c] >> s));
+                const uint32_t q = (((m >> 31) ^ (sb[c] >> s)) & 1u) |
+                                   ((m & MSA_META_NONE) == (er[c][s] & MSA_META_NONE) ? 2u : 0u);
+                cpk[c] |= q << (4 * s);
             }
+        }
         if (__builtin_expect(__ballot((anynan >> 29) & 3u) != 0ull, 0)) {
-            // a row with NaN at x_0 / x_1: |x_1| for the row's first edge, |x_0| for the others
+            // a row with NaN at x_0 / x_1: plane 3 (|x_1|) for the row's first edge, 2 (|x_0|) for the others
 #pragma unroll
             for (int c = 0; c < CPW; ++c)
 #pragma unroll
                 for (int s = 0; s < DV; ++s) {
-                    const uint32_t m = mw[c][s];
-                    const uint32_t eid = er[c][s] & MSA_META_NONE, rid = er[c][s] >> MSA_ER_SHIFT;
-                    const bool first = eid % DC == 0;  // edges are numbered row-major
-                    if ((m >> (first ? 30 : 29)) & 1u) {
-                        const double nv = rec[(((size_t)ty * M + rid) * MSA_REC_PLANES + (first ? 3 : 2)) * TILE + lane];
-                        l[c][s] = flip_sign(nv, (m >> 31) ^ (sb[c] >> s));
-                    }
+                    const bool first = (er[c][s] & MSA_META_NONE) % DC == 0;  // edges are numbered row-major
+                    if ((mw[c][s] >> (first ? 30 : 29)) & 1u)
+                        cpk[c] = (cpk[c] & ~(6u << (4 * s))) | ((first ? 3u : 2u) << (4 * s + 1));
                 }
         }
+#pragma unroll
+        for (int c = 0; c < CPW; ++c)
+#pragma unroll
+            for (int s = 0; s < DV; ++s) {
+                const int rid = (int)(er[c][s] >> MSA_ER_SHIFT);
+                const int sp = (int)((cpk[c] >> (4 * s + 1)) & 3u);
+                l[c][s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                         rrec, lane * 8 + sp * PB, rid * (MSA_REC_PLANES * PB), 0));
+            }
+#pragma unroll
+        for (int c = 0; c < CPW; ++c)
+#pragma unroll
+            for (int s = 0; s < DV; ++s) l[c][s] = flip_sign(l[c][s], cpk[c] >> (4 * s));
     }
     if (CONT && fl) {  // finished codeword: hard bits of its exit (ballots before this step's update)
         uint64_t hw[CPW];
