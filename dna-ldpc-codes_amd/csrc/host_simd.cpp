@@ -5,7 +5,6 @@
 // element, so they produce the same codes.
 #include "host_simd.hpp"
 
-#include <cmath>
 
 namespace ldpc {
 
@@ -21,7 +20,11 @@ __attribute__((target_clones("avx2", "default"))) bool host_encode_lattice(const
         const double x = src[i];
         const double kd = (x * inv + magic) - magic;
         bad |= (int)(kd * unit != x) | (int)!(kd <= lim && kd >= -lim);
-        code[i] = (int8_t)(int)std::fmin(std::fmax(kd, -lim), lim);
+        // clamp with plain compares (vectorise to blends; fmin / fmax would be
+        // library calls here): NaN becomes -lim, and such a value is flagged bad
+        double kc = kd >= -lim ? kd : -lim;
+        kc = kc <= lim ? kc : lim;
+        code[i] = (int8_t)(int)kc;
     }
     return bad == 0;
 }
