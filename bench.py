@@ -175,11 +175,11 @@ def algorithmic_bytes(eng, N, M, E) -> dict:
     8(d))."""
     if eng.msa_compressed:
         # compressed min-sum: the check phase reads E v->c fp64 and writes per
-        # row a {min1, min2} record + a 32-bit meta word (NaN planes only when
+        # row the min1 / min2 planes + a 16-bit meta word (NaN planes only when
         # NaN occurs); the variable phase reads the records and meta words,
         # N LLR and its columns' sign bytes, and writes E v->c fp64, the sign
         # bytes (N) and N/8 hard-bit ballots
-        return {"check": 8.0 * E + 20.0 * M, "variable": 8.0 * E + 20.0 * M + 10.0 * N + N / 8.0}
+        return {"check": 8.0 * E + 18.0 * M, "variable": 8.0 * E + 18.0 * M + 10.0 * N + N / 8.0}
     return {
         # check phase: read E v->c (d) + write E c->v (lr), fp64
         "check": 16.0 * E,
@@ -190,10 +190,10 @@ def algorithmic_bytes(eng, N, M, E) -> dict:
 
 def bound_detail(eng) -> str:
     if eng.msa_compressed:
-        return ("compressed min-sum (DESIGN.md sec. 4, 9): the check kernel streams its 4-tile group's v2c (302 MB, "
-                "more than the 256 MB Infinity Cache) from HBM; the variable kernel gathers the records and meta "
-                "words from its XCD's L2 and stores the fp64 v2c -- L2-request / issue bound rather than HBM-bound "
-                "(profiles/r3 PMC: L2 requests and VALU per wave); no MFMA")
+        return ("compressed min-sum (DESIGN.md sec. 4.2, 6.1): the check kernel streams its 4-tile group's v2c "
+                "(302 MB, more than the 256 MB Infinity Cache) from HBM; the variable kernel gathers the records and "
+                "meta words from its XCD's L2 and scatters the group's fp64 v2c back to HBM as 512-B nontemporal "
+                "segments, whose measured ceiling (ceiling_measured) bounds it; no MFMA")
     if eng.resident:
         return ("resident in-place pool sized to the 256 MB Infinity Cache: every message byte crosses the L2 -> "
                 "fabric interface once per phase (PMC fabric bytes = 1.02-1.04 x algorithmic), served by HBM and the "
@@ -233,14 +233,21 @@ def roofline(eng, G, st, cw_iters) -> dict:
     iter_bytes = (32.0 * E + 10.0 * N) * cw_iters
     per_cwi, traffic_src = find_traffic(names[dom])
     traffic = round(per_cwi * cw_iters / k_launch) if per_cwi else None
-    # measured ceiling of the access shape (tools/cachebench, profiles/r2/cachebench.txt): one launch per
-    # in-place pass of the check kernel's shape over a 192-224 MB working set (the resident pool's size)
-    ceiling = 6780.0 if eng.resident else None
+    # measured ceiling of the dominant kernel's access shape: the resident pool's in-place passes
+    # (tools/cachebench, profiles/r2/cachebench.txt: one launch per in-place pass of the check kernel's shape
+    # over a 192-224 MB working set), or the compressed min-sum variable kernel's v2c scatter (tools/wrbench,
+    # profiles/r3/wrbench_302MB.txt: 8 random 512-B nontemporal segments per wave over the group's 302 MB)
+    ceiling, ceiling_src = None, None
+    if eng.resident:
+        ceiling, ceiling_src = 6780.0, ("tools/cachebench: in-place 72 x 512 B per wave, one launch per pass, "
+                                        "192-224 MB working set (profiles/r2/cachebench.txt)")
+    elif eng.msa_compressed and dom == "variable":
+        ceiling, ceiling_src = 5090.0, ("tools/wrbench: 8 random 512-B nontemporal write segments per wave over "
+                                        "302 MB, the variable kernel's v2c scatter (profiles/r3/wrbench_302MB.txt)")
     return {
         "bound": "hbm", "kernel": names[dom], "bound_detail": bound_detail(eng),
         "ceiling_measured": ceiling,
-        "ceiling_source": ("tools/cachebench: in-place 72 x 512 B per wave, one launch per pass, 192-224 MB "
-                           "working set (profiles/r2/cachebench.txt)") if ceiling else None,
+        "ceiling_source": ceiling_src,
         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
         "frac_of_measured_ceiling": round(achieved / ceiling, 4) if (achieved and ceiling) else None,

@@ -136,15 +136,15 @@ static int upload(T** dst, const std::vector<T>& v)
 }
 
 // MSA-C scratch of `tiles` group tiles: record planes [tiles][M][4][64] fp64
-// (m1, m2, n0, n1), then the meta words [tiles][M][64] u32
+// (m1, m2, n0, n1), then the meta words [tiles][M][64] u16
 static size_t msa_scratch_bytes(int64_t tiles, int32_t M)
 {
-    return (size_t)tiles * M * dev::TILE * (dev::MSA_REC_PLANES * sizeof(double) + sizeof(uint32_t));
+    return (size_t)tiles * M * dev::TILE * (dev::MSA_REC_PLANES * sizeof(double) + sizeof(uint16_t));
 }
 static double* msa_rec(double* scratch) { return scratch; }
-static uint32_t* msa_meta(double* scratch, int64_t tiles, int32_t M)
+static uint16_t* msa_meta(double* scratch, int64_t tiles, int32_t M)
 {
-    return reinterpret_cast<uint32_t*>(scratch + (size_t)tiles * M * dev::MSA_REC_PLANES * dev::TILE);
+    return reinterpret_cast<uint16_t*>(scratch + (size_t)tiles * M * dev::MSA_REC_PLANES * dev::TILE);
 }
 
 int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, const ldpc_schedule* schedule)
@@ -162,8 +162,8 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     LDPC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
 
     const bool reg_72_8 = g->regular_dc && g->dc_max == 72 && g->regular_dv && g->dv_max == 8;
-    // compressed min-sum: 32-bit meta words carry edge ids (E < 2^18)
-    msa_c = algo == LDPC_ALGO_MSA && reg_72_8 && g->N % 16 == 0 && g->E < (int64_t)dev::MSA_META_NONE &&
+    // compressed min-sum: the packed column table carries edge ids (E < 2^18)
+    msa_c = algo == LDPC_ALGO_MSA && reg_72_8 && g->N % 16 == 0 && g->E < ((int64_t)1 << dev::MSA_ER_SHIFT) &&
             sched_flag(sched, LDPC_SCHED_MSA_COMPRESSED);
     cont = sched_flag(sched, LDPC_SCHED_CONTINUOUS) && !int_algo && reg_72_8;
     // resident pool: a few tiles whose whole state fits the
@@ -500,7 +500,7 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         if (N % (4 * cpw) != 0) cpw = 1;  // (N % 16 == 0: every CPW but 3 divides)
         const unsigned nb = gt * (unsigned)(N / (4 * cpw));
         const double* rec = msa_rec(scratch);
-        const uint32_t* meta = msa_meta(scratch, c2v_tiles, M);
+        const uint16_t* meta = msa_meta(scratch, c2v_tiles, M);
 #define VAR_MSA_C2(CONT, CPW, NT)                                                                                \
     klaunch((k_var_msa_c<72, 8, CONT, CPW, NT>), dim3(nb), dim3(256), 0, s, rec, meta, v2c, prior, hard, d_sgn, \
             active, d_col_er, pt, N, M, E, t0, (uint32_t)gt, rf)

@@ -912,6 +912,19 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
     }
 }
 
+// Raw buffer resource over [base, base + bytes) (gfx9 data format, no
+// swizzle, stride 0).  A wave's gathers and scatters then take a
+// wave-uniform byte offset in an SGPR (soffset) and one shared per-lane
+// offset in a VGPR: no per-edge 64-bit address arithmetic on the VALU.
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kBufNT = 2;  // cache-policy bits of a buffer access: nt (gfx950), as __builtin_nontemporal_store
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint64_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                            (int)(bytes < 0x7fffffffull ? bytes : 0x7fffffffull), 0x00020000);
+}
+
 // ---------------------------------------------------------------------------
 // Compressed min-sum check->variable messages ("MSA-C", (DC, DV)-regular
 // graphs with E < 2^18).  A row's DC outgoing messages take only four
@@ -919,9 +932,10 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
 // |x_0| or |x_1| -- and a sign, so the check phase writes per (row, lane):
 //   rec  [group tile][M][4][64] fp64 planes m1, m2, n0 = |x_0|, n1 = |x_1|
 //        (n0 / n1 written only when NaN)
-//   meta [group tile][M][64] u32: bit 31 the row's sign parity, bit 30 NaN at
-//        x_1, bit 29 NaN at x_0, bits 0-17 the edge id of min1 (row * DC +
-//        i1; MSA_META_NONE: no minimum, every |x| inf or NaN)
+//   meta [group tile][M][64] u16: bit 15 the row's sign parity, bit 14 NaN at
+//        x_1, bit 13 NaN at x_0, bit 12 no minimum (every |x| inf or NaN),
+//        bits 0-6 the low 7 bits of min1's edge id row * DC + i1 (unique
+//        within a row: DC <= 128 consecutive ids)
 // and nothing per edge.  The variable phase rebuilds each c2v from the meta
 // word, its own edge id and the sign bit of the v2c it stored itself (sgn,
 // !(x >= 0) of exactly that value -- the check's sign rule):
@@ -940,13 +954,14 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
 // slower (profiles/r3).
 // ---------------------------------------------------------------------------
 constexpr int MSA_REC_PLANES = 4;
-constexpr uint32_t MSA_META_NONE = 0x3ffffu;  // meta: no min1 (edge ids must stay below it)
+constexpr uint32_t MSA_META_ID = 0x7fu;      // meta bits 0-6: low bits of min1's edge id
+constexpr uint32_t MSA_META_NONE = 0x1000u;  // meta bit 12: no min1 (never equals an edge's low bits)
 
 // grid (ceil(M/4), group tiles), block 256: one wave per (row, tile); the
 // v2c group is streamed once (NT: nontemporal loads).
 template <int DC, bool NT>
 __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, double* __restrict__ rec,
-                                                     uint32_t* __restrict__ meta, const uint64_t* __restrict__ active,
+                                                     uint16_t* __restrict__ meta, const uint64_t* __restrict__ active,
                                                      int32_t M, int64_t E, int64_t t0)
 {
     static_assert(DC >= 2 && DC <= 96, "row degree");
@@ -956,10 +971,14 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     const uint64_t act = active[t];
     // whole-line policy (as k_check_msa)
     if (!(row < M && line_occupied(act, lane))) return;
-    const double* __restrict__ src = v2c + ((size_t)t * E + (size_t)row * DC) * TILE + lane;
+    // the row's DC segments through a buffer resource: per-edge offsets in
+    // the instructions, one per-lane VGPR offset (no 64-bit addresses)
+    const auto rv2c = buf_rsrc(v2c + ((size_t)t * E + (size_t)row * DC) * TILE, (uint64_t)DC * TILE * 8);
     double x[DC];
 #pragma unroll
-    for (int k = 0; k < DC; ++k) x[k] = ld<NT>(src + (size_t)k * TILE);
+    for (int k = 0; k < DC; ++k)
+        x[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv2c, lane * 8, k * (TILE * 8),
+                                                                               NT ? kBufNT : 0));
     // one pass: min1 with its FIRST index, min2 = minimum over the other
     // indices (a tie with min1 gives min2 == min1), NaN never compares less
     double m1 = __builtin_inf(), m2 = __builtin_inf();
@@ -988,8 +1007,8 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     if (nan0) r[2 * TILE] = a0;
     if (nan1) r[3 * TILE] = a1;
     meta[((size_t)blockIdx.y * M + row) * TILE + lane] =
-        (neg << 31) | ((nan1 ? 1u : 0u) << 30) | ((nan0 ? 1u : 0u) << 29) |
-        (i1 < 0 ? MSA_META_NONE : (uint32_t)(row * DC + i1));
+        (uint16_t)((neg << 15) | ((nan1 ? 1u : 0u) << 14) | ((nan0 ? 1u : 0u) << 13) |
+                   (i1 < 0 ? MSA_META_NONE : ((uint32_t)(row * DC + i1) & MSA_META_ID)));
 }
 
 __device__ __forceinline__ double flip_sign(double v, uint32_t neg)
@@ -997,23 +1016,17 @@ __device__ __forceinline__ double flip_sign(double v, uint32_t neg)
     return __longlong_as_double(__double_as_longlong(v) ^ ((long long)(neg & 1u) << 63));
 }
 
-// Raw buffer resource over [base, base + bytes) (gfx9 data format, no
-// swizzle, stride 0).  A wave's gathers and scatters then take a
-// wave-uniform byte offset in an SGPR (soffset) and one shared per-lane
-// offset in a VGPR: no per-edge 64-bit address arithmetic on the VALU.
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-constexpr int kBufNT = 2;  // cache-policy bits of a buffer access: nt (gfx950), as __builtin_nontemporal_store
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint64_t bytes)
-{
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
-                                            (int)(bytes < 0x7fffffffull ? bytes : 0x7fffffffull), 0x00020000);
-}
-
 // MSA-C column table: per CSC position q (column j's edges, ascending row),
 // (row of edge << 18) | edge id -- one wave-uniform word per edge (E < 2^18,
 // M < 2^14), so a wave's CPW x DV edges take CPW x DV SGPRs
 constexpr int MSA_ER_SHIFT = 18;
+constexpr uint32_t MSA_ER_EDGE = (1u << MSA_ER_SHIFT) - 1;
+// position of a packed column-table edge in its row (edges are numbered
+// row-major: id = row * DC + position); wave-uniform, scalar arithmetic
+__device__ __forceinline__ uint32_t er_pos(uint32_t er, int DC)
+{
+    return (er & MSA_ER_EDGE) - (er >> MSA_ER_SHIFT) * (uint32_t)DC;
+}
 
 // Min-sum variable phase on compressed messages (the arithmetic of k_var_m<MSA>).
 // 1-D grid of gt * (N / (4 CPW)) blocks; block L works on group tile L % gt.
@@ -1025,7 +1038,7 @@ constexpr int MSA_ER_SHIFT = 18;
 // resources (per-edge offsets in SGPRs); NT: nontemporal v2c stores (the
 // group's v2c is read back once, by the next check phase).
 template <int DC, int DV, bool CONT, int CPW, bool NT>
-__global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ rec, const uint32_t* __restrict__ meta,
+__global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ rec, const uint16_t* __restrict__ meta,
                                                    double* __restrict__ v2c,
                                                    double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                    uint8_t* __restrict__ sgn, const uint64_t* __restrict__ active,
@@ -1059,7 +1072,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
 #pragma unroll
         for (int s = 0; s < DV; ++s) er[c][s] = col_er[(size_t)(j0 + c) * DV + s];
     const auto rrec = buf_rsrc(rec + (size_t)ty * M * (MSA_REC_PLANES * TILE), (uint64_t)M * MSA_REC_PLANES * TILE * 8);
-    const auto rmeta = buf_rsrc(meta + (size_t)ty * M * TILE, (uint64_t)M * TILE * sizeof(uint32_t));
+    const auto rmeta = buf_rsrc(meta + (size_t)ty * M * TILE, (uint64_t)M * TILE * sizeof(uint16_t));
     const auto rv2c = buf_rsrc(v2c + (size_t)t * E * TILE, (uint64_t)E * TILE * sizeof(double));
     double l[CPW][DV], pv[CPW], xin[CPW];
     if (fr) {
@@ -1075,7 +1088,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
         // lane needs: the wave fetches the m1 plane's lines plus only the m2
         // lines holding a lane that needs them
         constexpr int PB = TILE * 8;  // bytes per record plane of one row
-        uint32_t sb[CPW], mw[CPW][DV], cpk[CPW];
+        uint32_t sb[CPW], mw[CPW][DV], cpk[CPW];  // mw: the u16 meta words
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             pv[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
@@ -1083,7 +1096,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
                 const int rid = (int)(er[c][s] >> MSA_ER_SHIFT);
-                mw[c][s] = __builtin_amdgcn_raw_buffer_load_b32(rmeta, lane * 4, rid * (TILE * 4), 0);
+                mw[c][s] = __builtin_amdgcn_raw_buffer_load_b16(rmeta, lane * 2, rid * (TILE * 2), 0);
             }
         }
         uint32_t anynan = 0;
@@ -1094,19 +1107,19 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             for (int s = 0; s < DV; ++s) {
                 const uint32_t m = mw[c][s];
                 anynan |= m;
-                const uint32_t q = (((m >> 31) ^ (sb[c] >> s)) & 1u) |
-                                   ((m & MSA_META_NONE) == (er[c][s] & MSA_META_NONE) ? 2u : 0u);
+                const uint32_t q = (((m >> 15) ^ (sb[c] >> s)) & 1u) |
+                                   ((m & (MSA_META_NONE | MSA_META_ID)) == (er[c][s] & MSA_META_ID) ? 2u : 0u);
                 cpk[c] |= q << (4 * s);
             }
         }
-        if (__builtin_expect(__ballot((anynan >> 29) & 3u) != 0ull, 0)) {
+        if (__builtin_expect(__ballot((anynan >> 13) & 3u) != 0ull, 0)) {
             // a row with NaN at x_0 / x_1: plane 3 (|x_1|) for the row's first edge, 2 (|x_0|) for the others
 #pragma unroll
             for (int c = 0; c < CPW; ++c)
 #pragma unroll
                 for (int s = 0; s < DV; ++s) {
-                    const bool first = (er[c][s] & MSA_META_NONE) % DC == 0;  // edges are numbered row-major
-                    if ((mw[c][s] >> (first ? 30 : 29)) & 1u)
+                    const bool first = er_pos(er[c][s], DC) == 0;
+                    if ((mw[c][s] >> (first ? 14 : 13)) & 1u)
                         cpk[c] = (cpk[c] & ~(6u << (4 * s))) | ((first ? 3u : 2u) << (4 * s + 1));
                 }
         }
@@ -1168,7 +1181,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             uint32_t sbn = 0;
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
-                const int eid = (int)(er[c][s] & MSA_META_NONE);
+                const int eid = (int)(er[c][s] & MSA_ER_EDGE);
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, dv[s]), rv2c, lane * 8,
                                                       eid * (TILE * 8), NT ? kBufNT : 0);
                 sbn |= (dv[s] >= 0 ? 0u : 1u) << s;

@@ -353,8 +353,8 @@ def test_continuous_batching_edge_cases(gpu, og, codewords, chunk):
                                                   (1, 4, 1, 3), (1, 2, 0, 3)])
 def test_min_sum_compressed_messages_bitexact(gpu, og, codewords, msa_c, group, cont, cpw):
     """MSA-C (kernels.hpp k_check_msa_c / k_var_msa_c): the check phase stores
-    per row a {min1, min2} record, a 32-bit meta word (sign parity, NaN at
-    x_0 / x_1, edge id of min1) and the NaN planes when needed; the variable
+    per row the min1 / min2 planes, a 16-bit meta word (sign parity, NaN at
+    x_0 / x_1, position of min1) and the NaN planes when needed; the variable
     phase rebuilds each c2v from them and the sign bits of the v2c it stored,
     so hard bits, iterations, valid flags and the posterior L stay bit-exact
     -- across group sizes (XCD-affine tile order, groups that do not divide

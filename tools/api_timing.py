@@ -12,6 +12,10 @@ import time
 
 import numpy as np
 
+if os.environ.get("API_TIMING_TORCH"):  # the bench.py process has torch and its HIP context up
+    import torch
+    torch.zeros(1, device="cuda")
+
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dna-ldpc-codes_amd"))
 import ldpc_amd as L  # noqa: E402
 import synth  # noqa: E402
