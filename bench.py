@@ -148,8 +148,9 @@ def cpu_baseline(args, og, llr_fn, B, gpu_out, cpus):
           "per_core": round(n / el / threads, 3),
           "host": cpus,
           "sample": f"{n} codewords of the same BSC(p={args.p}) workload (indices {start}..{start + n - 1}), "
-                    f"{args.max_iter} iters, oracle/ldpc_oracle.c on {threads} host threads (the affinity mask "
-                    f"{cpus['affinity']} capped by the cgroup CPU quota {cpus['cgroup_quota_cpus']}), {el:.1f} s"}
+                    f"{args.max_iter} iters, oracle/ldpc_oracle.c on {threads} host threads: every CPU this process "
+                    f"may use (the affinity mask lists {cpus['affinity']}, the cgroup CPU quota allows "
+                    f"{cpus['cgroup_quota_cpus']}; more threads than the quota only time-slice it), {el:.1f} s"}
     return cb, (c0 + c1, bad0 + bad1)
 
 
