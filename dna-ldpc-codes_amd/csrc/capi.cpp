@@ -480,7 +480,12 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
         // PCIe in double-buffered chunks of `xfer`.
         const int64_t sh64 = (shard + 63) / 64 * 64;
         const int64_t pool = o.chunk > 0 ? o.chunk : (shard <= kExplicitPoolMax ? sh64 : 0);
-        const int64_t xfer = std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool + 63) / 64 * 64));
+#ifndef LDPC_SMALL_SPLIT
+#define LDPC_SMALL_SPLIT 1
+#endif
+        const int64_t xfer = (o.chunk <= 0 && shard <= kExplicitPoolMax && LDPC_SMALL_SPLIT > 1)
+                                 ? ((shard + LDPC_SMALL_SPLIT - 1) / LDPC_SMALL_SPLIT + 63) / 64 * 64
+                                 : std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool + 63) / 64 * 64));
         std::unique_ptr<Slot> slot = g->take(dev, algo, pool, xfer, o.chunk <= 0 && pool > 0, sched);
         int rc = LDPC_OK;
         if (!slot) rc = make_slot(&g->h, dev, algo, pool, xfer, sched, slot);
@@ -492,7 +497,7 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
         Engine& E = *S.eng;
         const bool host_exp = (algo == LDPC_ALGO_BP) && o.exp_on_host;
         const int in_kind = (algo == LDPC_ALGO_BP && host_exp) ? LDPC_IN_LR : LDPC_IN_LLR;
-        const int64_t X = S.xfer, nch = (shard + X - 1) / X;
+        const int64_t X = xfer, nch = (shard + X - 1) / X;  // (the slot's staging holds >= xfer)
         auto c0 = [&](int64_t c) { return s0 + c * X; };
         auto cn = [&](int64_t c) { return std::min<int64_t>(X, s1 - c0(c)); };
         // host side of chunk c: exp (DNA_main.cpp:1344  g_received_LR[i] =

@@ -84,7 +84,8 @@ enum {
                                            the next one (fp64 decoders on (8,72)-regular graphs; default on;
                                            needs hard / iters / valid outputs) */
     LDPC_SCHED_MSA_COMPRESSED = 1 << 4, /* min-sum check->variable messages as per-row records (min1, min2,
-                                           NaN planes) + one 32-bit meta word per row (default on) */
+                                           NaN planes) + one 16-bit meta word per row and codeword
+                                           ((8,72)-regular graphs with E < 2^18; default on) */
     LDPC_SCHED_RESIDENT = 1 << 5,       /* continuous BP / fp64 min-sum: a pool of pool_tiles tiles iterated
                                            in place, its state sized to the 256 MB Infinity Cache, the
                                            syndrome fused into the check kernel (default on when the lane

@@ -6,6 +6,7 @@ of every call to stderr.
 
     LDPC_API_TIMING=1 python tools/api_timing.py default: t8:host_threads=8
 """
+import hashlib
 import os
 import sys
 import time
@@ -39,4 +40,6 @@ for spec in sys.argv[1:] or ["default:"]:
     if ref is None:
         ref = (h, it)
     assert np.array_equal(h, ref[0]) and np.array_equal(it, ref[1])
-    print(f"{name}: median {np.median(ts[2:]) * 1e3:.3f} ms, min {min(ts[2:]) * 1e3:.3f} ms", flush=True)
+    dig = hashlib.sha256(h.tobytes() + it.tobytes() + v.tobytes()).hexdigest()[:16]
+    print(f"{name}: median {np.median(ts[2:]) * 1e3:.3f} ms, min {min(ts[2:]) * 1e3:.3f} ms, outputs sha {dig}",
+          flush=True)
