@@ -11,7 +11,11 @@ rank decodes its own contiguous shard of `--batch-per-gpu` codewords
 --global-batch 1000000`), its dist.shard of [0, G), "scaling": "strong" --
 from the counter-based BSC(p=0.02) generator (transmitted word
 codeword_n18432_m1860_{1 + b mod 272}, LLR = +-ln49, LR = exp(LLR) by the
-host libm as DNA_main.cpp:1344 does).  p = 0.02 never converges, so every
+host libm as DNA_main.cpp:1344 does).  The channel output sits in HBM as one
+int8 code per bit (+-1, `--input code`, ldpc_engine_decode_codes with the
+table code -> code * ln49), the form the DNA pipeline's count differences take
+(decoder.py:314); `--input fp64` keeps fp64 LR / LLR values instead.  Both
+decode the same values bit for bit.  p = 0.02 never converges, so every
 codeword runs exactly 50 iterations.  Inputs are generated into HBM before the
 timed region; a step = one full decode of the shard (init, 50 x [syndrome,
 check, variable], final syndrome, hard-bit unpack, iteration counts).
@@ -84,6 +88,8 @@ def parse():
     ap.add_argument("--secondary", type=int, default=1,
                     help="N = 1: also time config 2 (DNA batch, host API) and config 5 (1M min-sum) after the headline")
     ap.add_argument("--msa-batch", type=int, default=1_000_000, help="config-5 secondary leg: codewords")
+    ap.add_argument("--input", default="code", choices=["code", "fp64"],
+                    help="channel output in HBM: int8 codes + a 256-entry table (default) or fp64 LR / LLR")
     ap.add_argument("--workload", default="bsc", choices=["bsc", "dna272"],
                     help="bsc: SURVEY 8(d) configs 3-5 (default); dna272: config 2, the 272-codeword DNA batch")
     return ap.parse_args()
@@ -154,21 +160,23 @@ def cpu_baseline(args, og, llr_fn, B, gpu_out, cpus):
     return cb, (c0 + c1, bad0 + bad1)
 
 
-def kernel_names(eng, algo) -> dict:
+def kernel_names(eng, algo, coded=False) -> dict:
     """Template instantiations of the check / variable kernels an engine
     launches (csrc/engine.hip launch_check / launch_var), as rocprofv3 names
-    them (tools/pmc_r3.py short form)."""
+    them (tools/pmc_r3.py short form); the variable kernels' last argument is
+    PC, coded priors (coded input on a continuous schedule)."""
     msa = "true" if algo == "msa" else "false"
+    pc = str(bool(coded) and eng.continuous).lower()
     if eng.msa_compressed:
         nt = str(eng.nontemporal).lower()
         return {"check": f"k_check_msa_c<72,{nt}>",
-                "variable": f"k_var_msa_c<72,8,{str(eng.continuous).lower()},{VAR_CPW},{nt}>"}
+                "variable": f"k_var_msa_c<72,8,{str(eng.continuous).lower()},{VAR_CPW},{nt},{pc}>"}
     chk = "k_check_msa" if algo == "msa" else "k_check_bp"
     if eng.resident:
-        return {"check": f"{chk}<72,false,true>", "variable": f"k_var_m<{msa},8,false,true,{VAR_CPW},true>"}
+        return {"check": f"{chk}<72,false,true>", "variable": f"k_var_m<{msa},8,false,true,{VAR_CPW},true,{pc}>"}
     nt = str(eng.nontemporal).lower()
     return {"check": f"{chk}<72,{nt},false>",
-            "variable": f"k_var_m<{msa},8,{nt},{str(eng.continuous).lower()},{VAR_CPW},false>"}
+            "variable": f"k_var_m<{msa},8,{nt},{str(eng.continuous).lower()},{VAR_CPW},false,{pc}>"}
 
 
 def algorithmic_bytes(eng, N, M, E) -> dict:
@@ -189,7 +197,14 @@ def algorithmic_bytes(eng, N, M, E) -> dict:
     }
 
 
-def bound_detail(eng) -> str:
+def bound_detail(eng, coded=False) -> str:
+    note = (" Coded input: the variable kernel reads each column's prior as a 1-byte code (+ a 2 KB table), "
+            "7 B per column and codeword-iteration fewer than the algorithmic (fp64 prior) bytes that `achieved` "
+            "counts." if coded and eng.continuous else "")
+    return _bound_detail(eng) + note
+
+
+def _bound_detail(eng) -> str:
     if eng.msa_compressed:
         return ("compressed min-sum (DESIGN.md sec. 4.2, 6.1): the check kernel streams its 4-tile group's v2c "
                 "(302 MB, more than the 256 MB Infinity Cache) from HBM; the variable kernel gathers the records and "
@@ -215,12 +230,12 @@ def find_traffic(kname):
     return None, None
 
 
-def roofline(eng, G, st, cw_iters) -> dict:
+def roofline(eng, G, st, cw_iters, coded=False) -> dict:
     """Roofline of the dominant kernel: algorithmic bytes per launch / its
     average launch duration (HIP events on the kernel's dispatch packet)."""
     N, M, E = G.N, G.M, G.E
     by_kernel = algorithmic_bytes(eng, N, M, E)
-    names = kernel_names(eng, "msa" if eng.algo == 1 else "bp")
+    names = kernel_names(eng, "msa" if eng.algo == 1 else "bp", coded)
 
     def avg_ms(k):
         return st[k]["ms"] / st[k]["sampled"] if st[k]["sampled"] else 0.0
@@ -246,7 +261,7 @@ def roofline(eng, G, st, cw_iters) -> dict:
         ceiling, ceiling_src = 5090.0, ("tools/wrbench: 8 random 512-B nontemporal write segments per wave over "
                                         "302 MB, the variable kernel's v2c scatter (profiles/r3/wrbench_302MB.txt)")
     return {
-        "bound": "hbm", "kernel": names[dom], "bound_detail": bound_detail(eng),
+        "bound": "hbm", "kernel": names[dom], "bound_detail": bound_detail(eng, coded),
         "ceiling_measured": ceiling,
         "ceiling_source": ceiling_src,
         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -327,6 +342,27 @@ def dna272(args, og, threads, max_iter=200):
     return out
 
 
+def channel(L, eng, args, dev, N, b0, B, d_cw, n_cw, p, kind):
+    """The BSC channel output of codewords [b0, b0 + B) in HBM -- int8 codes
+    with the table code -> code * ln49 (--input code) or fp64 values of `kind`
+    -- and the decode call on it."""
+    import synth
+    if args.input == "code":
+        d_in = L.DeviceBuffer(dev, B * N)
+        eng.gen_bsc_codes(d_in.at(0), b0, B, d_cw.at(0), n_cw, args.seed, p)
+        table = np.arange(-128, 128, dtype=np.float64) * synth.LLR_UNIT
+
+        def decode(Bx, max_iter, h, it, v):
+            eng.decode_codes(d_in.at(0), table, L.IN_LLR, Bx, max_iter, h, None, L.POST_LLR, it, v)
+    else:
+        d_in = L.DeviceBuffer(dev, B * N * 8)
+        eng.gen_bsc(d_in.at(0), kind, b0, B, d_cw.at(0), n_cw, args.seed, p, synth.LLR_UNIT)
+
+        def decode(Bx, max_iter, h, it, v):
+            eng.decode(d_in.at(0), kind, Bx, max_iter, h, None, L.POST_LLR, it, v)
+    return d_in, decode
+
+
 def msa_1m(args, og, threads, cw, d_cw):
     """Config 5: min-sum (Run_MSA_Decoder_INF) with early termination on
     `--msa-batch` codewords of BSC(p = 0.002), 1 warm-up + 2 timed decodes,
@@ -337,12 +373,11 @@ def msa_1m(args, og, threads, cw, d_cw):
     N = G.N
     B, p, max_iter = args.msa_batch, 0.002, 50
     eng = L.Engine(G, 0, "msa")
-    d_in = L.DeviceBuffer(0, B * N * 8)
-    eng.gen_bsc(d_in.at(0), L.IN_LLR, 0, B, d_cw.at(0), cw.shape[0], args.seed, p, synth.LLR_UNIT)
+    d_in, decode = channel(L, eng, args, 0, N, 0, B, d_cw, cw.shape[0], p, L.IN_LLR)
     d_hard, d_iters, d_valid = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
 
     def step():
-        eng.decode(d_in.at(0), L.IN_LLR, B, max_iter, d_hard.at(0), None, L.POST_LLR, d_iters.at(0), d_valid.at(0))
+        decode(B, max_iter, d_hard.at(0), d_iters.at(0), d_valid.at(0))
 
     step()
     eng.sync()
@@ -357,11 +392,11 @@ def msa_1m(args, og, threads, cw, d_cw):
     iters = d_iters.download(np.empty(B, np.int32))
     valid = d_valid.download(np.empty(B, np.uint8))
     cw_iters = float(iters.sum()) * steps
-    out = {"workload": f"bsc-p{p}-{B // 1000}k-msa{max_iter}", "batch": B, "steps": steps,
+    out = {"workload": f"bsc-p{p}-{B // 1000}k-msa{max_iter}", "batch": B, "steps": steps, "input": args.input,
            "value": round(B * steps / el, 1), "unit": "codewords/s", "ms_per_step": round(el / steps * 1e3, 2),
            "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 5),
            "resident_per_pass": eng.cap, "group_tiles": eng.group_tiles, "compressed_msa": eng.msa_compressed,
-           "roofline": roofline(eng, G, st, cw_iters)}
+           "roofline": roofline(eng, G, st, cw_iters, args.input == "code")}
     if og is not None:
         n = max(8, 4 * threads)
 
@@ -434,16 +469,14 @@ def main():
     d_cw = L.DeviceBuffer(dev, cw.nbytes)
     d_cw.upload(cw)
     in_kind = L.IN_LR if algo == "bp" else L.IN_LLR
-    d_in = L.DeviceBuffer(dev, B * N * 8)
-    eng.gen_bsc(d_in.at(0), in_kind, b0, B, d_cw.at(0), cw.shape[0], args.seed, args.p, synth.LLR_UNIT)
+    d_in, decode = channel(L, eng, args, dev, N, b0, B, d_cw, cw.shape[0], args.p, in_kind)
     d_hard = L.DeviceBuffer(dev, B * N)
     d_iters = L.DeviceBuffer(dev, B * 4)
     d_valid = L.DeviceBuffer(dev, B)
     eng.sync()
 
     def step():
-        eng.decode(d_in.at(0), in_kind, B, args.max_iter, d_hard.at(0), None, L.POST_LLR, d_iters.at(0),
-                   d_valid.at(0))
+        decode(B, args.max_iter, d_hard.at(0), d_iters.at(0), d_valid.at(0))
 
     for _ in range(args.warmup):
         step()
@@ -481,6 +514,8 @@ def main():
         "config": {"workload": (f"bsc-p{args.p}-{args.global_batch // 1000}k-global-{algo}{args.max_iter}"
                                 if args.global_batch > 0 else f"bsc-p{args.p}-{B // 1000}k-per-gpu-{algo}{args.max_iter}"),
                    "code": "decode_n18432_m2048_final.pchk (8,72)-regular, E=147456",
+                   "input": ("int8 channel codes in HBM + table code*ln49 (LR = host exp)" if args.input == "code"
+                             else "fp64 LR / LLR in HBM"),
                    "batch_per_gpu": B, "per_rank": per_rank, "global_batch": int(round(total_cw / args.steps)),
                    "max_iter": args.max_iter,
                    "algo": algo, "parallelism": f"dp{world} (contiguous codeword shards, no collective)",
@@ -488,7 +523,7 @@ def main():
                    "continuous": eng.continuous, "resident_pool": eng.resident,
                    "compressed_msa": eng.msa_compressed, "syndrome_split": eng.syndrome_split,
                    "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 4)},
-        "roofline": roofline(eng, G, st, cw_iters),
+        "roofline": roofline(eng, G, st, cw_iters, args.input == "code"),
     }
 
     # ---- correctness of the timed decode: every rank checks its own shard ----

@@ -108,10 +108,13 @@ class Workers {
     bool stop_ = false;
 };
 
-// LR table path (DNA batches): an LLR that is an exact multiple k * unit, |k|
-// <= kCodeMax, gets LR = table[k] = the host libm's exp(k * unit) -- the same
-// bits as exp(LLR), DNA_main.cpp:1344 -- and crosses PCIe as one byte.
+// Code table path (DNA batches): an LLR that is an exact multiple k * unit,
+// |k| <= kCodeMax, crosses PCIe as the byte k and the engine decodes the codes
+// (Engine::decode_codes) with table[k + 128] = k * unit: BP's LR is the host
+// libm's exp of that value -- the same bits as exp(LLR), DNA_main.cpp:1344 --
+// and min-sum reads the value itself.
 constexpr int kCodeMax = 127;
+constexpr int kTable = 256;
 
 // the unit: the smallest nonzero |LLR| among the chunk's first rows (a guess;
 // every value is checked against it)
@@ -171,10 +174,10 @@ struct Slot {
     uint8_t* d_valid[2] = {};
     uint8_t* h_hbits[2] = {};  // hard bits packed 8 per byte (N % 8 == 0)
     uint8_t* d_hbits[2] = {};
-    int8_t* h_code[2] = {};   // LR table path: one byte per LLR
+    int8_t* h_code[2] = {};   // code table path: one byte per LLR
     int8_t* d_code[2] = {};
-    double* h_table[2] = {};  // [2 * kCodeMax + 1]
-    double* d_table[2] = {};
+    std::vector<double> h_table[2];  // [kTable] LLR of code k at k + 128
+    bool coded[2] = {};              // the staging buffer holds codes (else fp64 input)
     std::unique_ptr<Workers> workers;
 
     ~Slot()
@@ -183,9 +186,9 @@ struct Slot {
         if (eng) hipSetDevice(device);
         for (int k = 0; k < 2; k++) {
             hipHostFree(h_in[k]); hipHostFree(h_post[k]); hipHostFree(h_hard[k]); hipHostFree(h_iters[k]);
-            hipHostFree(h_valid[k]); hipHostFree(h_code[k]); hipHostFree(h_table[k]); hipHostFree(h_hbits[k]);
+            hipHostFree(h_valid[k]); hipHostFree(h_code[k]); hipHostFree(h_hbits[k]);
             hipFree(d_in[k]); hipFree(d_post[k]); hipFree(d_hard[k]); hipFree(d_iters[k]); hipFree(d_valid[k]);
-            hipFree(d_code[k]); hipFree(d_table[k]); hipFree(d_hbits[k]);
+            hipFree(d_code[k]); hipFree(d_hbits[k]);
             if (ev_h2d[k]) hipEventDestroy(ev_h2d[k]);
             if (ev_dec[k]) hipEventDestroy(ev_dec[k]);
             if (ev_d2h[k]) hipEventDestroy(ev_d2h[k]);
@@ -236,11 +239,10 @@ int make_slot(const HostGraph* g, int device, int algo, int64_t pool, int64_t xf
             LDPC_HIP(hipHostMalloc((void**)&s->h_hbits[k], C * N / 8, hipHostMallocDefault));
             LDPC_HIP(hipMalloc((void**)&s->d_hbits[k], C * N / 8));
         }
-        if (algo == LDPC_ALGO_BP) {
+        if (algo == LDPC_ALGO_BP || algo == LDPC_ALGO_MSA) {
             LDPC_HIP(hipHostMalloc((void**)&s->h_code[k], C * N, hipHostMallocDefault));
             LDPC_HIP(hipMalloc((void**)&s->d_code[k], C * N));
-            LDPC_HIP(hipHostMalloc((void**)&s->h_table[k], (2 * kCodeMax + 1) * sizeof(double), hipHostMallocDefault));
-            LDPC_HIP(hipMalloc((void**)&s->d_table[k], (2 * kCodeMax + 1) * sizeof(double)));
+            s->h_table[k].assign(kTable, 0.0);
         }
     }
     out = std::move(s);
@@ -480,12 +482,7 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
         // PCIe in double-buffered chunks of `xfer`.
         const int64_t sh64 = (shard + 63) / 64 * 64;
         const int64_t pool = o.chunk > 0 ? o.chunk : (shard <= kExplicitPoolMax ? sh64 : 0);
-#ifndef LDPC_SMALL_SPLIT
-#define LDPC_SMALL_SPLIT 1
-#endif
-        const int64_t xfer = (o.chunk <= 0 && shard <= kExplicitPoolMax && LDPC_SMALL_SPLIT > 1)
-                                 ? ((shard + LDPC_SMALL_SPLIT - 1) / LDPC_SMALL_SPLIT + 63) / 64 * 64
-                                 : std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool + 63) / 64 * 64));
+const int64_t xfer = std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool + 63) / 64 * 64));
         std::unique_ptr<Slot> slot = g->take(dev, algo, pool, xfer, o.chunk <= 0 && pool > 0, sched);
         int rc = LDPC_OK;
         if (!slot) rc = make_slot(&g->h, dev, algo, pool, xfer, sched, slot);
@@ -510,9 +507,9 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
             LDPC_HIP(hipSetDevice(dev));
             if (c >= 2) LDPC_HIP(hipEventSynchronize(S.ev_h2d[k]));  // staging buffer free again
             const double tp0 = api_timing ? now() : 0;
-            // LR table path: all of the chunk's LLRs exact multiples of one unit
+            // code table path: all of the chunk's LLRs exact multiples of one unit
             bool coded = false;
-            if (host_exp && lr_table && S.h_code[k]) {
+            if ((host_exp || algo == LDPC_ALGO_MSA) && lr_table && S.h_code[k]) {
                 const double unit = llr_unit(src, Bc, N);
                 if (unit > 0) {
                     // in pieces, each crossing PCIe while the next is encoded
@@ -530,7 +527,7 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
                                                     (size_t)(p1 - p0) * N, hipMemcpyHostToDevice, S.copy));
                     }
                     if (ok) {
-                        for (int q = -kCodeMax; q <= kCodeMax; q++) S.h_table[k][q + kCodeMax] = std::exp((double)q * unit);
+                        for (int q = -kCodeMax; q <= kCodeMax; q++) S.h_table[k][q + 128] = (double)q * unit;
                         coded = true;
                     }
                 }
@@ -547,19 +544,15 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
             }
             const double tp1 = api_timing ? now() : 0;
             if (c >= 2) LDPC_HIP(hipStreamWaitEvent(S.copy, S.ev_dec[k], 0));
-            if (coded) {  // (the codes are on their way already)
-                LDPC_HIP(hipMemcpyAsync(S.d_table[k], S.h_table[k], (2 * kCodeMax + 1) * sizeof(double),
-                                        hipMemcpyHostToDevice, S.copy));
-                int r = E.expand_lr(S.d_code[k], S.d_table[k], S.d_in[k], Bc * (int64_t)N, S.copy);
-                if (r) return r;
-            } else {
+            S.coded[k] = coded;
+            if (!coded) {  // (codes are on their way already; their table goes with the decode)
                 LDPC_HIP(hipMemcpyAsync(S.d_in[k], S.h_in[k], (size_t)Bc * N * 8, hipMemcpyHostToDevice, S.copy));
             }
             LDPC_HIP(hipEventRecord(S.ev_h2d[k], S.copy));
             if (api_timing) {
                 LDPC_HIP(hipEventSynchronize(S.ev_h2d[k]));
-                std::fprintf(stderr, "api chunk %lld: %s %.3f ms, + H2D%s %.3f ms\n", (long long)c,
-                             coded ? "encode" : "exp/copy", tp1 - tp0, coded ? " + expand" : "", now() - tp1);
+                std::fprintf(stderr, "api chunk %lld: %s %.3f ms, + H2D %.3f ms\n", (long long)c,
+                             coded ? "encode" : "exp/copy", tp1 - tp0, now() - tp1);
             }
             return LDPC_OK;
         };
@@ -603,8 +596,10 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
             E.tie_base = c0(c);  // tie hash keyed by the codeword's index in this call
             LDPC_HIP(hipStreamWaitEvent(E.stream, S.ev_h2d[k], 0));
             const double td0 = api_timing ? now() : 0;
-            int r = E.decode(S.d_in[k], in_kind, Bc, max_iter, S.d_hard[k], post_out ? S.d_post[k] : nullptr,
-                             o.post_kind, S.d_iters[k], S.d_valid[k]);
+            int r = S.coded[k] ? E.decode_codes(S.d_code[k], S.h_table[k].data(), LDPC_IN_LLR, Bc, max_iter, S.d_hard[k],
+                                                post_out ? S.d_post[k] : nullptr, o.post_kind, S.d_iters[k], S.d_valid[k])
+                               : E.decode(S.d_in[k], in_kind, Bc, max_iter, S.d_hard[k],
+                                          post_out ? S.d_post[k] : nullptr, o.post_kind, S.d_iters[k], S.d_valid[k]);
             if (r) return r;
             if (api_timing)
                 std::fprintf(stderr, "api chunk %lld: decode enqueue + drain wait %.3f ms\n", (long long)c, now() - td0);
@@ -710,6 +705,14 @@ int ldpc_engine_decode(ldpc_engine* e, const double* d_in, int32_t in_kind, int6
     return e->e->decode(d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
 }
 
+int ldpc_engine_decode_codes(ldpc_engine* e, const int8_t* d_codes, const double* table, int32_t table_kind,
+                             int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post, int32_t post_kind,
+                             int32_t* d_iters, uint8_t* d_valid)
+{
+    if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
+    return e->e->decode_codes(d_codes, table, table_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
+}
+
 int ldpc_engine_sync(ldpc_engine* e)
 {
     if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
@@ -725,6 +728,13 @@ int ldpc_engine_gen_bsc(ldpc_engine* e, double* d_out, int32_t out_kind, int64_t
 {
     if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
     return e->e->gen_bsc(d_out, out_kind, b0, B, d_codewords, n_cw, seed, p, llr_mag);
+}
+
+int ldpc_engine_gen_bsc_codes(ldpc_engine* e, int8_t* d_out, int64_t b0, int64_t B, const uint8_t* d_codewords,
+                              int32_t n_cw, uint64_t seed, double p)
+{
+    if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
+    return e->e->gen_bsc_codes(d_out, b0, B, d_codewords, n_cw, seed, p);
 }
 
 int ldpc_engine_profile(ldpc_engine* e, int32_t stride)

@@ -123,6 +123,8 @@ Engine::~Engine()
     hipFree(d_sgn);
     hipFree(v2c); if (c2v != v2c) hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
     hipFree(post_t);
+    hipFree(pcode); hipFree(d_ptab); hipFree(d_expand);
+    if (h_ptab) hipHostFree(h_ptab);
     if (stream) hipStreamDestroy(stream);
 }
 
@@ -456,32 +458,37 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
     return LDPC_OK;
 }
 
-template <bool MSA, bool NT, bool CONT, bool INPLACE>
+template <bool MSA, bool NT, bool CONT, bool INPLACE, bool PC = false>
 static void var_m_cpw(int cpw, hipStream_t s, dim3 grid, const double* c2v, double* v2c, double* prior, uint64_t* hard,
                       const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N, int64_t E, int64_t t0,
                       const dev::Refill& rf)
 {
     using namespace dev;
     if (cpw == 8)
-        klaunch((k_var_m<MSA, 8, NT, CONT, 8, INPLACE>), grid, dim3(256), 0, s, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+        klaunch((k_var_m<MSA, 8, NT, CONT, 8, INPLACE, PC>), grid, dim3(256), 0, s, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
     else if (cpw == 4)
-        klaunch((k_var_m<MSA, 8, NT, CONT, 4, INPLACE>), grid, dim3(256), 0, s, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+        klaunch((k_var_m<MSA, 8, NT, CONT, 4, INPLACE, PC>), grid, dim3(256), 0, s, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
     else if (cpw == 2)
-        klaunch((k_var_m<MSA, 8, NT, CONT, 2, INPLACE>), grid, dim3(256), 0, s, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+        klaunch((k_var_m<MSA, 8, NT, CONT, 2, INPLACE, PC>), grid, dim3(256), 0, s, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
     else
-        klaunch((k_var_m<MSA, 8, NT, CONT, 1, INPLACE>), grid, dim3(256), 0, s, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+        klaunch((k_var_m<MSA, 8, NT, CONT, 1, INPLACE, PC>), grid, dim3(256), 0, s, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
 }
 
+// PC: coded priors (continuous refills only: rf.in_code set)
 template <bool MSA>
 static void var_m(bool nt, bool cont, bool inplace, int cpw, hipStream_t s, dim3 grid, const double* c2v, double* v2c,
                   double* prior, uint64_t* hard, const uint64_t* active, const int32_t* col_edge, double* pt, int32_t N,
                   int64_t E, int64_t t0, const dev::Refill& rf)
 {
+    const bool pc = cont && rf.in_code != nullptr;
     // in place (the resident pool, or its placement probe) is never nontemporal
-    if (inplace && cont) var_m_cpw<MSA, false, true, true>(cpw, s, grid, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+    if (inplace && pc) var_m_cpw<MSA, false, true, true, true>(cpw, s, grid, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+    else if (inplace && cont) var_m_cpw<MSA, false, true, true>(cpw, s, grid, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
     else if (inplace) var_m_cpw<MSA, false, false, true>(cpw, s, grid, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+    else if (nt && pc) var_m_cpw<MSA, true, true, false, true>(cpw, s, grid, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
     else if (nt && cont) var_m_cpw<MSA, true, true, false>(cpw, s, grid, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
     else if (nt) var_m_cpw<MSA, true, false, false>(cpw, s, grid, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
+    else if (pc) var_m_cpw<MSA, false, true, false, true>(cpw, s, grid, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
     else if (cont) var_m_cpw<MSA, false, true, false>(cpw, s, grid, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
     else var_m_cpw<MSA, false, false, false>(cpw, s, grid, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
 }
@@ -501,9 +508,14 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         const unsigned nb = gt * (unsigned)(N / (4 * cpw));
         const double* rec = msa_rec(scratch);
         const uint16_t* meta = msa_meta(scratch, c2v_tiles, M);
-#define VAR_MSA_C2(CONT, CPW, NT)                                                                                \
-    klaunch((k_var_msa_c<72, 8, CONT, CPW, NT>), dim3(nb), dim3(256), 0, s, rec, meta, v2c, prior, hard, d_sgn, \
+#define VAR_MSA_C3(CONT, CPW, NT, PC)                                                                                \
+    klaunch((k_var_msa_c<72, 8, CONT, CPW, NT, PC>), dim3(nb), dim3(256), 0, s, rec, meta, v2c, prior, hard, d_sgn, \
             active, d_col_er, pt, N, M, E, t0, (uint32_t)gt, rf)
+#define VAR_MSA_C2(CONT, CPW, NT)                                   \
+    do {                                                            \
+        if (CONT && rf.in_code) VAR_MSA_C3(CONT, CPW, NT, CONT);    \
+        else VAR_MSA_C3(CONT, CPW, NT, false);                      \
+    } while (0)
 #define VAR_MSA_C(CONT, CPW)              \
     do {                                  \
         if (nt_d) VAR_MSA_C2(CONT, CPW, true); \
@@ -521,6 +533,7 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         });
 #undef VAR_MSA_C
 #undef VAR_MSA_C2
+#undef VAR_MSA_C3
         return LDPC_OK;
     }
     if (reg8) {
@@ -666,6 +679,61 @@ int Engine::run_chunk_int(const double* d_in, int64_t Bc, int64_t b_base, int32_
     return LDPC_OK;
 }
 
+// Coded input.  The continuous schedules keep every lane's prior as its code
+// (1 byte per column and lane instead of 8; the kernels look the value up in
+// the 256-entry table); the others decode fp64 input expanded from the codes
+// one pass of <= cap codewords at a time.  Either way each codeword sees
+// exactly the prior values the table gives its codes.
+int Engine::decode_codes(const int8_t* d_codes, const double* h_table, int table_kind, int64_t B, int32_t max_iter,
+                         uint8_t* d_hard, double* d_post, int post_kind, int32_t* d_iters, uint8_t* d_valid)
+{
+    if (B < 0 || max_iter < 0) { set_error("B and max_iter must be >= 0"); return LDPC_ERR_ARG; }
+    if (!h_table || (B > 0 && !d_codes)) { set_error("decode_codes: null codes or table"); return LDPC_ERR_ARG; }
+    if (table_kind != LDPC_IN_LLR && table_kind != LDPC_IN_LR) { set_error("table kind: LDPC_IN_LLR or LDPC_IN_LR"); return LDPC_ERR_ARG; }
+    const bool bp = algo == LDPC_ALGO_BP;
+    if (!bp && table_kind != LDPC_IN_LLR) { set_error("min-sum and the integer decoders take an LLR table"); return LDPC_ERR_ARG; }
+    if (B == 0) return LDPC_OK;
+    LDPC_HIP(hipSetDevice(device));
+    constexpr int T = 256;
+    // the prior of code k: BP's LR (the host libm exp of an LLR table, as
+    // DNA_main.cpp:1344 computes LR), the LLR otherwise
+    double tab[T];
+    for (int i = 0; i < T; i++) tab[i] = (bp && table_kind == LDPC_IN_LLR) ? std::exp(h_table[i]) : h_table[i];
+    if (!d_ptab) {
+        LDPC_HIP(hipMalloc((void**)&d_ptab, T * sizeof(double)));
+        LDPC_HIP(hipHostMalloc((void**)&h_ptab, T * sizeof(double), hipHostMallocDefault));
+    }
+    if (!ptab_valid || std::memcmp(tab, h_ptab, sizeof tab) != 0) {
+        // the previous upload (and every kernel that reads the table) done first
+        LDPC_HIP(hipStreamSynchronize(stream));
+        std::memcpy(h_ptab, tab, sizeof tab);
+        LDPC_HIP(hipMemcpyAsync(d_ptab, h_ptab, sizeof tab, hipMemcpyHostToDevice, stream));
+        ptab_valid = true;
+    }
+    const int in_kind = bp ? LDPC_IN_LR : LDPC_IN_LLR;
+    if (cont && algo < LDPC_ALGO_QMSA) {
+        if (!pcode) LDPC_HIP(hipMalloc((void**)&pcode, (size_t)cap * g->N));
+        cur_codes = d_codes;
+        const int rc = run_cont(nullptr, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
+        cur_codes = nullptr;
+        return rc;
+    }
+    const size_t N = (size_t)g->N;
+    if (!d_expand) LDPC_HIP(hipMalloc((void**)&d_expand, (size_t)cap * N * sizeof(double)));
+    const int64_t tb = tie_base;
+    for (int64_t b0 = 0; b0 < B; b0 += cap) {
+        const int64_t Bc = std::min<int64_t>(cap, B - b0);
+        if (int rc = expand_lr(d_codes + (size_t)b0 * N, d_ptab, d_expand, Bc * (int64_t)N, stream)) return rc;
+        tie_base = tb + b0;  // the integer decoders' tie hash keys on the index in the whole call
+        const int rc = decode(d_expand, in_kind, Bc, max_iter, d_hard ? d_hard + (size_t)b0 * N : nullptr,
+                              d_post ? d_post + (size_t)b0 * N : nullptr, post_kind, d_iters ? d_iters + b0 : nullptr,
+                              d_valid ? d_valid + b0 : nullptr);
+        tie_base = tb;
+        if (rc) return rc;
+    }
+    return LDPC_OK;
+}
+
 int Engine::decode(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
                    int post_kind, int32_t* d_iters, uint8_t* d_valid)
 {
@@ -769,8 +837,14 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     const uint64_t q0 = poll_seq;  // this decode's first poll
     ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, ContOut{d_iters, d_valid}};
     const int hard_vec = ((uintptr_t)d_hard % 8 == 0 && N % 8 == 0) ? 1 : 0;
-    const Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
-                    d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
+    Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
+              d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
+    if (cur_codes) {  // coded input (decode_codes): int8 priors
+        rf.in = nullptr;
+        rf.in_code = cur_codes;
+        rf.pcode = pcode;
+        rf.ptab = d_ptab;
+    }
     // A batch that fits the lane pool in one fill (the DNA batch) polls one
     // step behind instead of kLag: its steps take >= 30 us, time enough to
     // enqueue the next, and the decode ends one empty step sooner.
@@ -846,8 +920,12 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             const unsigned gt = (unsigned)std::min<int64_t>(gstep, tiles - t0);
             int rc;
             if (ffp && s == 1) {
-                LAUNCH(K_CHECK, klaunch((k_check_bp_first<72>), dim3((M + 3) / 4, gt), dim3(256), 0, stream, prior,
-                                        d_col_idx, c2v, active, M, N, (int64_t)g->E, t0));
+                if (cur_codes)
+                    LAUNCH(K_CHECK, klaunch((k_check_bp_first<72, true>), dim3((M + 3) / 4, gt), dim3(256), 0, stream,
+                                            prior, pcode, d_ptab, d_col_idx, c2v, active, M, N, (int64_t)g->E, t0));
+                else
+                    LAUNCH(K_CHECK, klaunch((k_check_bp_first<72>), dim3((M + 3) / 4, gt), dim3(256), 0, stream,
+                                            prior, pcode, d_ptab, d_col_idx, c2v, active, M, N, (int64_t)g->E, t0));
             } else if (s == 0) {
                 // step 0: the reset left every lane empty and the syndrome
                 // launch above only claims codewords, so no lane is active
@@ -878,8 +956,20 @@ int Engine::gen_bsc(double* d_out, int out_kind, int64_t b0, int64_t B, const ui
         neg = std::exp(-llr_mag);
     }
     const uint64_t seedmix = dev::splitmix64(seed);
-    LAUNCH(K_OTHER, klaunch(dev::k_gen_bsc, dim3(8192), dim3(256), 0, stream, d_out, out_kind == LDPC_IN_LR ? 1 : 0,
-                            b0, B, d_cw, n_cw, g->N, seedmix, p, pos, neg));
+    LAUNCH(K_OTHER, klaunch(dev::k_gen_bsc<double>, dim3(8192), dim3(256), 0, stream, d_out,
+                            out_kind == LDPC_IN_LR ? 1 : 0, b0, B, d_cw, n_cw, g->N, seedmix, p, pos, neg));
+    return LDPC_OK;
+}
+
+int Engine::gen_bsc_codes(int8_t* d_out, int64_t b0, int64_t B, const uint8_t* d_cw, int32_t n_cw, uint64_t seed,
+                          double p)
+{
+    if (B <= 0) return LDPC_OK;
+    if (n_cw <= 0 || !d_cw || !d_out) { set_error("gen_bsc_codes: bad arguments"); return LDPC_ERR_ARG; }
+    LDPC_HIP(hipSetDevice(device));
+    const uint64_t seedmix = dev::splitmix64(seed);
+    LAUNCH(K_OTHER, klaunch(dev::k_gen_bsc<int8_t>, dim3(8192), dim3(256), 0, stream, d_out, 0, b0, B, d_cw, n_cw,
+                            g->N, seedmix, p, (int8_t)1, (int8_t)-1));
     return LDPC_OK;
 }
 

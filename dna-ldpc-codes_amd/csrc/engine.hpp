@@ -92,6 +92,16 @@ struct Engine {
     int32_t* iters = nullptr;
     uint8_t* valid = nullptr;
     double* post_t = nullptr;  // [tiles][N][64] per-iteration posterior (allocated on first use)
+    // coded input (decode_codes): the lanes' int8 prior codes [tiles][N][64],
+    // the prior table (256 fp64, code + 128), its last uploaded contents (an
+    // unchanged table is not re-sent), the fp64 staging of schedules without
+    // coded kernels, and the input codes of the decode in progress
+    int8_t* pcode = nullptr;
+    double* d_ptab = nullptr;
+    double* h_ptab = nullptr;
+    bool ptab_valid = false;
+    double* d_expand = nullptr;
+    const int8_t* cur_codes = nullptr;
     // integer decoders (LDPC_ALGO_QMSA / GALLAGER_*): int32 views of v2c, c2v, prior
     int32_t q_precision = 6, q_beta = 0;
     double q_step = 0.5;
@@ -115,16 +125,23 @@ struct Engine {
                   int post_kind, int32_t* d_iters, uint8_t* d_valid);
     int decode(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
                int post_kind, int32_t* d_iters, uint8_t* d_valid);
+    // coded input: d_codes [B][N] int8 on device, h_table[256] (host) the
+    // channel value of code k at k + 128, of kind table_kind (LDPC_IN_LLR or,
+    // BP only, LDPC_IN_LR); BP takes the host exp of an LLR table
+    int decode_codes(const int8_t* d_codes, const double* h_table, int table_kind, int64_t B, int32_t max_iter,
+                     uint8_t* d_hard, double* d_post, int post_kind, int32_t* d_iters, uint8_t* d_valid);
     // integer decoders, Bc <= cap codewords; b_base = global index of the first (tie hash)
     int run_chunk_int(const double* d_in, int64_t Bc, int64_t b_base, int32_t max_iter, uint8_t* d_hard,
                       double* d_post, int32_t* d_iters, uint8_t* d_valid);
     int set_params(int32_t precision, double step, int32_t beta, uint64_t seed);
     int gen_bsc(double* d_out, int out_kind, int64_t b0, int64_t B, const uint8_t* d_cw, int32_t n_cw, uint64_t seed,
                 double p, double llr_mag);
+    // the same channel as int8 codes: +1 for a received 0, -1 for a 1
+    int gen_bsc_codes(int8_t* d_out, int64_t b0, int64_t B, const uint8_t* d_cw, int32_t n_cw, uint64_t seed, double p);
     int collect_stats();
     // LDPC_SCHED_* bits in effect (ldpc_engine_info)
     int32_t flags() const;
-    // out[i] = table[code[i] + 127] for i < n on stream s (host-API input path)
+    // out[i] = table[code[i] + 128] for i < n on stream s
     int expand_lr(const int8_t* d_code, const double* d_table, double* d_out, int64_t n, hipStream_t s);
     // out[i] bit r = in[8 i + r] for i < nbytes on the engine stream (host-API hard-bit copy)
     int pack_bits(const uint8_t* d_in, uint8_t* d_out, int64_t nbytes);

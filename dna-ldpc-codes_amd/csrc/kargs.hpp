@@ -26,7 +26,17 @@ struct Refill {
     // single fill (every lane refilled at once, none live): store only the
     // prior; the next check derives d0 = 1 - 2/(1+LR) from it (k_check_bp_first)
     int prior_only = 0;
+    // coded input (ldpc_engine_decode_codes): the input is int8 channel codes
+    // [B][N] (in_code, `in` unused) and every lane keeps its prior as the code
+    // ([tile][N][64] pcode) instead of fp64; the prior value of code k is
+    // ptab[k + 128] (LR for BP, LLR for min-sum)
+    const int8_t* in_code = nullptr;
+    int8_t* pcode = nullptr;
+    const double* ptab = nullptr;
 };
+
+// prior value of a code (coded input): table indexed by code + 128
+constexpr int kCodeBias = 128;
 
 struct ContState {
     uint64_t* active;      // [tile] lanes updated by check/variable this step

@@ -474,8 +474,11 @@ __device__ __forceinline__ void check_bp_block(typename Msg<RES>::in dmsg, typen
 // the refill (Init_Belief_Propagation dec.cpp:608-629 + the stored d of
 // dec.cpp:652) -- gathered from the tile's [N][64] prior instead of read from
 // E stored copies; then k_check_bp's arithmetic.  Same grid as k_check_bp.
-template <int DC>
+// PC: the prior is the lanes' int8 codes (pcode) and the LR table (ptab).
+template <int DC, bool PC = false>
 __global__ __launch_bounds__(256, 2) void k_check_bp_first(const double* __restrict__ prior,
+                                                           const int8_t* __restrict__ pcode,
+                                                           const double* __restrict__ ptab,
                                                            const int32_t* __restrict__ col_idx,
                                                            double* __restrict__ lr, const uint64_t* __restrict__ active,
                                                            int32_t M, int32_t N, int64_t E, int64_t t0)
@@ -485,11 +488,19 @@ __global__ __launch_bounds__(256, 2) void k_check_bp_first(const double* __restr
     const int64_t t = t0 + blockIdx.y;
     const uint64_t act = active[t];
     if (!(row < M && line_occupied(act, lane))) return;
-    const double* __restrict__ pt = prior + (size_t)t * N * TILE + lane;
+    const size_t pt = (size_t)t * N * TILE + lane;
     const int32_t* __restrict__ cols = col_idx + (size_t)row * DC;
     double x[DC];
+    if constexpr (PC) {
+        int8_t k8[DC];
 #pragma unroll
-    for (int k = 0; k < DC; ++k) x[k] = pt[(size_t)cols[k] * TILE];
+        for (int k = 0; k < DC; ++k) k8[k] = pcode[pt + (size_t)cols[k] * TILE];
+#pragma unroll
+        for (int k = 0; k < DC; ++k) x[k] = ptab[k8[k] + kCodeBias];
+    } else {
+#pragma unroll
+        for (int k = 0; k < DC; ++k) x[k] = prior[pt + (size_t)cols[k] * TILE];
+    }
 #pragma unroll
     for (int k = 0; k < DC; ++k) x[k] = 1.0 - 2.0 / (1.0 + x[k]);
     check_bp_compute<DC, false>(x, lr + ((size_t)blockIdx.y * E + (size_t)row * DC) * TILE + lane);
@@ -535,6 +546,16 @@ __global__ __launch_bounds__(256) void k_check_bp_gen(const double* __restrict__
     }
 }
 
+// A lane's prior at [tile][N][64] index i: the fp64 value, or with PC (coded
+// input) the table value of its int8 code -- 1 byte per column and lane moves
+// instead of 8; the table (2 KB) stays in the L1 / L2.
+template <bool PC>
+__device__ __forceinline__ double prior_at(const double* __restrict__ prior, const Refill& rf, size_t i)
+{
+    if constexpr (PC) return rf.ptab[rf.pcode[i] + kCodeBias];
+    else return prior[i];
+}
+
 // ---------------------------------------------------------------------------
 // Variable-node phase, regular column degree DV, CPW consecutive columns per
 // wave (every c2v load of the wave's columns is issued before the first
@@ -553,9 +574,11 @@ __global__ __launch_bounds__(256) void k_check_bp_gen(const double* __restrict__
 // CONT: refilled lanes (Refill::fresh) get Init_Belief_Propagation
 // (dec.cpp:608-629) / Init_MSA_INF (dec.cpp:1300-1329) through the same
 // stores, and finished lanes (Refill::fin) get their outputs written first.
-// INPLACE: v2c == c2v (resident pool), see Msg.
+// INPLACE: v2c == c2v (resident pool), see Msg.  PC (coded input, CONT
+// only): the lanes' priors are int8 codes (Refill::pcode / ptab), refills
+// read the input's codes (Refill::in_code).
 // Column block cb (4 waves x CPW columns) of tile t; c2v_t = the tile's c2v messages.
-template <bool MSA, int DV, bool NT, bool CONT, int CPW, bool INPLACE>
+template <bool MSA, int DV, bool NT, bool CONT, int CPW, bool INPLACE, bool PC = false>
 __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typename Msg<INPLACE>::out v2c,
                                             double* __restrict__ prior, uint64_t* __restrict__ hard,
                                             const uint64_t* __restrict__ active, const int32_t* __restrict__ col_edge,
@@ -588,17 +611,27 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
 #pragma unroll
         for (int s = 0; s < DV; ++s) eid[c][s] = col_edge[(size_t)(j0 + c) * DV + s];
     double l[CPW][DV], pv[CPW], xin[CPW];
+    int8_t kin[CPW];  // PC: the refilled lane's input codes
     if (fr) {  // refilled lane: its input row, prefetched with the c2v loads
-        const double* __restrict__ in_row = rf.in + (size_t)rf.lane_b[t * TILE + lane] * N;
+        const size_t rb = (size_t)rf.lane_b[t * TILE + lane] * N;
 #pragma unroll
-        for (int c = 0; c < CPW; ++c) xin[c] = in_row[j0 + c];
+        for (int c = 0; c < CPW; ++c) {
+            if constexpr (PC) kin[c] = rf.in_code[rb + j0 + c];
+            else xin[c] = rf.in[rb + j0 + c];
+        }
     }
     if (live) {
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
-            pv[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
+            pv[c] = prior_at<PC>(prior, rf, ((size_t)t * N + j0 + c) * TILE + lane);
 #pragma unroll
             for (int s = 0; s < DV; ++s) l[c][s] = c2v_t[(size_t)eid[c][s] * TILE + lane];
+        }
+    }
+    if constexpr (PC) {
+        if (fr) {
+#pragma unroll
+            for (int c = 0; c < CPW; ++c) xin[c] = rf.ptab[kin[c] + kCodeBias];
         }
     }
     if (CONT && fl) {  // finished codeword: hard bits of its exit (ballots before this step's update)
@@ -613,7 +646,7 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
         const size_t pj = ((size_t)t * N + j) * TILE + lane;
         if (CONT && fl && rf.post_out) {  // finished codeword: posterior of its exit
             const size_t ob = (size_t)fb * N + j;
-            const double pv = fn > 0 ? post[pj] : prior[pj];
+            const double pv = fn > 0 ? post[pj] : prior_at<PC>(prior, rf, pj);
             if (MSA) rf.post_out[ob] = pv;
             else {
                 const double P = __builtin_isnan(pv) ? 1.0 : pv;
@@ -634,7 +667,8 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
                 for (int s = 0; s < DV; ++s) dv[s] = x;
                 h = !(x > 0);
             } else {
-                const double LR0 = rf.in_is_llr ? exp(x) : x;
+                // PC: the table holds LR already (the host exp of the caller's LLR table)
+                const double LR0 = (!PC && rf.in_is_llr) ? exp(x) : x;
                 np = LR0;
                 const double d0 = 1.0 - 2.0 / (1.0 + LR0);
 #pragma unroll
@@ -674,7 +708,10 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
                 }
             }
         }
-        if (CONT && fr) prior[pj] = np;
+        if (CONT && fr) {
+            if constexpr (PC) rf.pcode[pj] = kin[c];
+            else prior[pj] = np;
+        }
         // whole-line stores (others write 0, never read) -- not in a tile that
         // only hands out finished codewords (no live or refilled lane), nor
         // for refills whose first check reads the prior (Refill::prior_only)
@@ -692,14 +729,15 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
     }
 }
 
-template <bool MSA, int DV, bool NT, bool CONT, int CPW, bool INPLACE>
+template <bool MSA, int DV, bool NT, bool CONT, int CPW, bool INPLACE, bool PC = false>
 __global__ __launch_bounds__(256) void k_var_m(typename Msg<INPLACE>::in c2v, typename Msg<INPLACE>::out v2c,
                                                double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                const uint64_t* __restrict__ active,
                                                const int32_t* __restrict__ col_edge, double* __restrict__ post,
                                                int32_t N, int64_t E, int64_t t0, Refill rf)
 {
-    var_m_block<MSA, DV, NT, CONT, CPW, INPLACE>(c2v + (size_t)blockIdx.y * E * TILE, v2c, prior, hard, active,
+    static_assert(CONT || !PC, "coded priors come with continuous refills");
+    var_m_block<MSA, DV, NT, CONT, CPW, INPLACE, PC>(c2v + (size_t)blockIdx.y * E * TILE, v2c, prior, hard, active,
                                                  col_edge, post, N, E, t0 + blockIdx.y,
                                                  xcd_block(blockIdx.x, gridDim.x), rf);
 }
@@ -1036,8 +1074,9 @@ __device__ __forceinline__ uint32_t er_pos(uint32_t er, int DC)
 // them.  The meta loads of the wave's CPW columns go out together, then the
 // record loads (their plane depends on the meta word), all through buffer
 // resources (per-edge offsets in SGPRs); NT: nontemporal v2c stores (the
-// group's v2c is read back once, by the next check phase).
-template <int DC, int DV, bool CONT, int CPW, bool NT>
+// group's v2c is read back once, by the next check phase).  PC: coded
+// priors, as k_var_m.
+template <int DC, int DV, bool CONT, int CPW, bool NT, bool PC = false>
 __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ rec, const uint16_t* __restrict__ meta,
                                                    double* __restrict__ v2c,
                                                    double* __restrict__ prior, uint64_t* __restrict__ hard,
@@ -1074,11 +1113,16 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
     const auto rrec = buf_rsrc(rec + (size_t)ty * M * (MSA_REC_PLANES * TILE), (uint64_t)M * MSA_REC_PLANES * TILE * 8);
     const auto rmeta = buf_rsrc(meta + (size_t)ty * M * TILE, (uint64_t)M * TILE * sizeof(uint16_t));
     const auto rv2c = buf_rsrc(v2c + (size_t)t * E * TILE, (uint64_t)E * TILE * sizeof(double));
+    static_assert(CONT || !PC, "coded priors come with continuous refills");
     double l[CPW][DV], pv[CPW], xin[CPW];
+    int8_t kin[CPW];  // PC: the refilled lane's input codes
     if (fr) {
-        const double* __restrict__ in_row = rf.in + (size_t)rf.lane_b[t * TILE + lane] * N;
+        const size_t rb = (size_t)rf.lane_b[t * TILE + lane] * N;
 #pragma unroll
-        for (int c = 0; c < CPW; ++c) xin[c] = in_row[j0 + c];
+        for (int c = 0; c < CPW; ++c) {
+            if constexpr (PC) kin[c] = rf.in_code[rb + j0 + c];
+            else xin[c] = rf.in[rb + j0 + c];
+        }
     }
     if (live) {
         // the meta words first; from them, per edge a 4-bit code (bit 0: the
@@ -1091,7 +1135,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
         uint32_t sb[CPW], mw[CPW][DV], cpk[CPW];  // mw: the u16 meta words
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
-            pv[c] = prior[((size_t)t * N + j0 + c) * TILE + lane];
+            pv[c] = prior_at<PC>(prior, rf, ((size_t)t * N + j0 + c) * TILE + lane);
             sb[c] = sgn[((size_t)t * N + j0 + c) * TILE + lane];
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
@@ -1149,14 +1193,14 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
         const size_t pj = ((size_t)t * N + j) * TILE + lane;
         if (CONT && fl && rf.post_out) {  // finished codeword: posterior L of its exit
             const size_t ob = (size_t)fb * N + j;
-            rf.post_out[ob] = fn > 0 ? post[pj] : prior[pj];
+            rf.post_out[ob] = fn > 0 ? post[pj] : prior_at<PC>(prior, rf, pj);
         }
         bool h = false;
         double dv[DV];
 #pragma unroll
         for (int s = 0; s < DV; ++s) dv[s] = 0.0;
         if (fr) {  // Init_MSA_INF for a refilled lane
-            const double x = xin[c];
+            const double x = PC ? rf.ptab[kin[c] + kCodeBias] : xin[c];
 #pragma unroll
             for (int s = 0; s < DV; ++s) dv[s] = x;
             h = !(x > 0);
@@ -1176,7 +1220,10 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             h = !(P > 0);
             if (post) post[pj] = P;
         }
-        if (CONT && fr) prior[pj] = xin[c];
+        if (CONT && fr) {
+            if constexpr (PC) rf.pcode[pj] = kin[c];
+            else prior[pj] = xin[c];
+        }
         if (line_occupied(touched, lane) || fr || live) {  // whole-line stores, as k_var_m
             uint32_t sbn = 0;
 #pragma unroll
@@ -1345,10 +1392,10 @@ __global__ __launch_bounds__(256) void k_lr_table(const int8_t* __restrict__ cod
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8; q += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t c = reinterpret_cast<const uint64_t*>(code)[q];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) out[q * 8 + r] = table[(int)(int8_t)(c >> (8 * r)) + 127];
+        for (int r = 0; r < 8; ++r) out[q * 8 + r] = table[(int)(int8_t)(c >> (8 * r)) + kCodeBias];
     }
     for (int64_t i = n8 * 8 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = table[(int)code[i] + 127];
+        out[i] = table[(int)code[i] + kCodeBias];
 }
 
 // ---------------------------------------------------------------------------
@@ -1357,9 +1404,11 @@ __global__ __launch_bounds__(256) void k_lr_table(const int8_t* __restrict__ cod
 //   flip = u * 2^-53 < p;  y = codeword[b mod n_cw][j] ^ flip
 //   LLR = y ? -mag : +mag   (LR: y ? lr_neg : lr_pos, host-exp'd)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gen_bsc(double* __restrict__ out, int out_lr, int64_t b0, int64_t B,
+// T = int8_t: the channel as codes (+1 / -1, coded input)
+template <typename T>
+__global__ __launch_bounds__(256) void k_gen_bsc(T* __restrict__ out, int out_lr, int64_t b0, int64_t B,
                                                  const uint8_t* __restrict__ cws, int32_t n_cw, int32_t N,
-                                                 uint64_t seedmix, double p, double pos, double negv)
+                                                 uint64_t seedmix, double p, T pos, T negv)
 {
     const int64_t total = B * (int64_t)N;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {

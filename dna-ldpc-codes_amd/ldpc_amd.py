@@ -133,7 +133,7 @@ EXPORTS = [
     "ldpc_graph_load_alist", "ldpc_graph_rs_ldpc", "ldpc_graph_save_pchk", "ldpc_graph_save_alist",
     "ldpc_graph_free", "ldpc_graph_info", "ldpc_graph_blocks", "ldpc_graph_edges", "ldpc_graph_syndrome", "ldpc_decode",
     "ldpc_engine_create", "ldpc_engine_create_ex", "ldpc_engine_info", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
-    "ldpc_engine_gen_bsc", "ldpc_engine_set_params", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
+    "ldpc_engine_decode_codes", "ldpc_engine_gen_bsc", "ldpc_engine_gen_bsc_codes", "ldpc_engine_set_params", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
     "ldpc_dev_memcpy", "ldpc_dna_llr", "ldpc_dna_edit_distance", "ldpc_write_soft_files", "ldpc_py_float_repr",
 ]
 
@@ -181,10 +181,12 @@ def lib():
         L.ldpc_engine_free.argtypes = [vp]
         L.ldpc_engine_free.restype = None
         L.ldpc_engine_decode.argtypes = [vp, vp, i32, i64, i32, vp, vp, i32, vp, vp]
+        L.ldpc_engine_decode_codes.argtypes = [vp, vp, vp, i32, i64, i32, vp, vp, i32, vp, vp]
         L.ldpc_engine_sync.argtypes = [vp]
         L.ldpc_engine_stream.argtypes = [vp]
         L.ldpc_engine_stream.restype = vp
         L.ldpc_engine_gen_bsc.argtypes = [vp, vp, i32, i64, i64, vp, i32, C.c_uint64, dbl, dbl]
+        L.ldpc_engine_gen_bsc_codes.argtypes = [vp, vp, i64, i64, vp, i32, C.c_uint64, dbl]
         L.ldpc_engine_profile.argtypes = [vp, i32]
         L.ldpc_engine_set_params.argtypes = [vp, i32, dbl, i32, C.c_uint64]
         L.ldpc_engine_stats.argtypes = [vp, C.POINTER(KernelStats)]
@@ -542,12 +544,25 @@ class Engine:
         _check(lib().ldpc_engine_decode(self._h, d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters,
                                         d_valid))
 
+    def decode_codes(self, d_codes, table: np.ndarray, table_kind: int, B: int, max_iter: int, d_hard=None,
+                     d_post=None, post_kind=POST_LLR, d_iters=None, d_valid=None):
+        """Decode int8 channel codes [B][N] (device) with table[code + 128] the
+        channel value of a code (ldpc_engine_decode_codes)."""
+        t = np.ascontiguousarray(table, dtype=np.float64)
+        if t.shape != (256,):
+            raise ValueError("the code table has 256 entries (code + 128)")
+        _check(lib().ldpc_engine_decode_codes(self._h, d_codes, _ptr(t), table_kind, B, max_iter, d_hard, d_post,
+                                              post_kind, d_iters, d_valid))
+
     def set_params(self, msa_precision: int = 6, msa_step: float = 0.5, msa_offset: int = 0, tie_seed: int = 0):
         """Quantized min-sum parameters (Set_MSA dec.cpp:1683)."""
         _check(lib().ldpc_engine_set_params(self._h, msa_precision, msa_step, msa_offset, tie_seed))
 
     def gen_bsc(self, d_out, out_kind: int, b0: int, B: int, d_cw, n_cw: int, seed: int, p: float, llr_mag: float):
         _check(lib().ldpc_engine_gen_bsc(self._h, d_out, out_kind, b0, B, d_cw, n_cw, seed, p, llr_mag))
+
+    def gen_bsc_codes(self, d_out, b0: int, B: int, d_cw, n_cw: int, seed: int, p: float):
+        _check(lib().ldpc_engine_gen_bsc_codes(self._h, d_out, b0, B, d_cw, n_cw, seed, p))
 
     def sync(self):
         _check(lib().ldpc_engine_sync(self._h))

@@ -228,6 +228,19 @@ void ldpc_engine_free(ldpc_engine *e);
 int ldpc_engine_decode(ldpc_engine *e, const double *d_in, int32_t in_kind, int64_t B, int32_t max_iter,
                        uint8_t *d_hard, double *d_post, int32_t post_kind, int32_t *d_iters, uint8_t *d_valid);
 
+/* The same decode for channel outputs given as small integers -- the DNA
+ * pipeline's per-bit count differences k, whose LLR is k * ln((1-eps)/eps)
+ * (decoder.py:314), or a BSC's +-1: d_codes [B][N] int8 on the device and
+ * table[256] (host) the channel value of code k at table[k + 128], of kind
+ * table_kind (LDPC_IN_LLR; LDPC_IN_LR for BP only).  BP takes LR = the host
+ * libm exp of an LLR table entry, as DNA_main.cpp:1344 does per bit.  The
+ * result equals ldpc_engine_decode on the fp64 input table[code + 128]
+ * bit for bit; the continuous schedules keep each codeword's prior as its
+ * one-byte code instead of an fp64 value. */
+int ldpc_engine_decode_codes(ldpc_engine *e, const int8_t *d_codes, const double *table, int32_t table_kind,
+                             int64_t B, int32_t max_iter, uint8_t *d_hard, double *d_post, int32_t post_kind,
+                             int32_t *d_iters, uint8_t *d_valid);
+
 int ldpc_engine_sync(ldpc_engine *e);
 
 /* The engine's HIP stream (hipStream_t as void*). */
@@ -241,6 +254,12 @@ void *ldpc_engine_stream(ldpc_engine *e);
  * [B][N] fp64. */
 int ldpc_engine_gen_bsc(ldpc_engine *e, double *d_out, int32_t out_kind, int64_t b0, int64_t B,
                         const uint8_t *d_codewords, int32_t n_cw, uint64_t seed, double p, double llr_mag);
+
+/* The same channel as codes for ldpc_engine_decode_codes: d_out [B][N] int8,
+ * +1 where the received bit is 0 and -1 where it is 1 (table[129] = llr_mag,
+ * table[127] = -llr_mag gives ldpc_engine_gen_bsc's LLRs). */
+int ldpc_engine_gen_bsc_codes(ldpc_engine *e, int8_t *d_out, int64_t b0, int64_t B, const uint8_t *d_codewords,
+                              int32_t n_cw, uint64_t seed, double p);
 
 /* Kernel timing: HIP events on the engine stream around every stride-th
  * launch of each kernel class (stride 1 = every launch, 0 = off).  Enabling

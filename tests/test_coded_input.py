@@ -1,0 +1,151 @@
+"""Coded channel input (ldpc_engine_decode_codes, the host API's code table path).
+
+The DNA pipeline's soft input is a per-bit count difference k with LLR =
+k * ln 49 (decoder.py:314); a BSC's is +-1 * ln 49.  Decoding the int8 codes
+with a 256-entry table must give exactly what decoding the fp64 values
+table[k + 128] gives -- BP's LR being the host exp of the LLR
+(DNA_main.cpp:1344) -- on every schedule: the continuous ones keep each lane's
+prior as its code (kernels.hpp prior_at / Refill::pcode), the others expand the
+codes to fp64 first.
+"""
+import numpy as np
+import pytest
+
+import synth
+from conftest import PCHK
+
+pytestmark = pytest.mark.gpu
+
+
+def _table(unit=synth.LLR_UNIT):
+    return np.arange(-128, 128, dtype=np.float64) * unit
+
+
+def _run(L, eng, B, N, fn):
+    dh, dit, dv = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
+    dp = L.DeviceBuffer(0, B * N * 8)
+    fn(dh.at(0), dp.at(0), dit.at(0), dv.at(0))
+    eng.sync()
+    return (dh.download(np.empty((B, N), np.uint8)), dp.download(np.empty((B, N), np.float64)),
+            dit.download(np.empty(B, np.int32)), dv.download(np.empty(B, np.uint8)))
+
+
+def _same(a, b):
+    for x, y in zip(a, b):
+        assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+
+
+def test_device_bsc_codes_match_llrs(gpu, G, codewords):
+    L = gpu
+    eng = L.Engine(G, 0, "bp", chunk=64)
+    B, N = 90, G.N
+    cw = L.DeviceBuffer(0, codewords.nbytes)
+    cw.upload(codewords)
+    out = L.DeviceBuffer(0, B * N)
+    eng.gen_bsc_codes(out.at(0), 4321, B, cw.at(0), 272, 2026, 0.02)
+    eng.sync()
+    codes = out.download(np.empty((B, N), np.int8))
+    assert set(np.unique(codes)) <= {-1, 1}
+    exp = synth.bsc_llrs(codewords, 4321, B, seed=2026, p=0.02)
+    assert np.array_equal(_table()[codes.astype(np.int64) + 128], exp)
+
+
+# (algo, schedule, chunk): the resident BP pool, the grouped continuous BP
+# schedule with a single fill (first check from the prior), fixed passes, the
+# compressed and the fp64 continuous min-sum, and the quantized min-sum
+CASES = [("bp", {}, 0), ("bp", dict(resident=False), 0), ("bp", dict(resident=False), 320),
+         ("bp", dict(continuous=False), 128), ("msa", {}, 0), ("msa", dict(msa_compressed=False), 0),
+         ("msa", dict(continuous=False), 0), ("qmsa", {}, 128)]
+
+
+@pytest.mark.parametrize("algo,sch,chunk", CASES)
+def test_coded_equals_fp64_input(gpu, G, codewords, algo, sch, chunk):
+    """decode_codes == decode on the expanded fp64 input, bit for bit: hard
+    bits, posterior, iterations, valid flags (BSC codes generated on the device,
+    and DNA count differences with erasures uploaded from the host)."""
+    L = gpu
+    N = G.N
+    cw = L.DeviceBuffer(0, codewords.nbytes)
+    cw.upload(codewords)
+    p = 0.004 if algo == "bp" else 0.002
+    B = 300
+    eng = L.Engine(G, 0, algo, chunk=chunk, schedule=sch)
+    codes = L.DeviceBuffer(0, B * N)
+    eng.gen_bsc_codes(codes.at(0), 0, B, cw.at(0), 272, 2026, p)
+    fp = L.DeviceBuffer(0, B * N * 8)
+    bp = algo == "bp"
+    kind = L.IN_LR if bp else L.IN_LLR
+    eng.gen_bsc(fp.at(0), kind, 0, B, cw.at(0), 272, 2026, p, synth.LLR_UNIT)
+    tab = _table()
+    post = L.POST_RATIO if bp else L.POST_LLR
+    a = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode_codes(codes.at(0), tab, L.IN_LLR, B, 40, h, pp, post, it, v))
+    b = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode(fp.at(0), kind, B, 40, h, pp, post, it, v))
+    _same(a, b)
+    assert len(np.unique(a[2])) > 2
+    # DNA count differences (erasures k = 0 included), one fill of the pool
+    llr = synth.dna_like_llrs(codewords, seed=4, reads=58000)[:150]
+    k = np.rint(llr / synth.LLR_UNIT).astype(np.int8)
+    assert np.array_equal(k.astype(np.float64) * synth.LLR_UNIT, llr)
+    B = len(k)
+    codes.upload(k)
+    fp.upload(np.exp(llr) if bp else llr)
+    a = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode_codes(codes.at(0), tab, L.IN_LLR, B, 60, h, pp, post, it, v))
+    b = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode(fp.at(0), kind, B, 60, h, pp, post, it, v))
+    _same(a, b)
+
+
+def test_coded_lr_table_and_oracle(gpu, G, og, codewords):
+    """An LR table (BP) equals the LLR table's host exp, and the coded decode
+    equals the oracle; a min-sum engine refuses an LR table."""
+    L = gpu
+    N = G.N
+    llr = synth.dna_like_llrs(codewords, seed=9, reads=56000)[:130]
+    k = np.rint(llr / synth.LLR_UNIT).astype(np.int8)
+    B = len(k)
+    codes = L.DeviceBuffer(0, B * N)
+    codes.upload(k)
+    eng = L.Engine(G, 0, "bp")
+    a = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode_codes(codes.at(0), _table(), L.IN_LLR, B, 60, h, pp,
+                                                                 L.POST_RATIO, it, v))
+    b = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode_codes(codes.at(0), np.exp(_table()), L.IN_LR, B, 60, h,
+                                                                 pp, L.POST_RATIO, it, v))
+    _same(a, b)
+    rh, rp, rit, rv = og.decode_batch(llr, 60, algo=0, post_mode=1, threads=8)
+    assert np.array_equal(a[0], rh) and np.array_equal(a[2], rit) and np.array_equal(a[3], rv)
+    assert np.array_equal(a[1].view(np.uint64), rp.view(np.uint64))
+    em = L.Engine(G, 0, "msa")
+    with pytest.raises(L.LdpcError):
+        em.decode_codes(codes.at(0), np.exp(_table()), L.IN_LR, B, 10)
+
+
+def test_host_api_min_sum_code_path(G, og, codewords):
+    """ldpc_decode sends lattice LLR batches as codes for min-sum too (capi.cpp
+    code table path): equal to the oracle and to the fp64 path (lr_table off)."""
+    llr = synth.bsc_llrs(codewords, 0, 200, seed=2026, p=0.002)
+    ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, 50, algo=1, post_mode=0, threads=8)
+    for lt in (True, False):
+        h, p, it, v = G.decode(llr, max_iter=50, algo="msa", post="llr", schedule=dict(lr_table=lt))
+        assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
+        assert np.array_equal(p.view(np.uint64), ref_p.view(np.uint64))
+
+
+def test_changing_tables_between_decodes(gpu, codewords):
+    """Back-to-back coded decodes with different tables on one engine: each
+    sees its own table (the upload waits for the decodes that read the last)."""
+    L = gpu
+    G2 = L.Graph(PCHK)
+    N = G2.N
+    llr = synth.dna_like_llrs(codewords, seed=10, reads=57000)[:64]
+    k = np.rint(llr / synth.LLR_UNIT).astype(np.int8)
+    codes = L.DeviceBuffer(0, k.nbytes)
+    codes.upload(k)
+    eng = L.Engine(G2, 0, "bp")
+    outs = []
+    for unit in (synth.LLR_UNIT, 0.7, synth.LLR_UNIT):
+        outs.append(_run(L, eng, 64, N, lambda h, pp, it, v: eng.decode_codes(
+            codes.at(0), _table(unit), L.IN_LLR, 64, 30, h, pp, L.POST_RATIO, it, v)))
+    _same(outs[0], outs[2])
+    assert not np.array_equal(outs[0][1], outs[1][1])
+    ref = G2.decode(k.astype(np.float64) * 0.7, max_iter=30, post="ratio", schedule=dict(lr_table=False))
+    assert np.array_equal(outs[1][0], ref[0]) and np.array_equal(outs[1][2], ref[2])
+    assert np.array_equal(outs[1][1].view(np.uint64), ref[1].view(np.uint64))
