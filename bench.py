@@ -283,10 +283,12 @@ def roofline(eng, G, st, cw_iters, coded=False) -> dict:
 
 def dna272(args, og, threads, max_iter=200):
     """Config 2: the 272-codeword DNA-like batch (synth.dna_like_llrs, 72000
-    reads) at the pipeline's max_iter, device-resident (LR = host libm exp,
-    DNA_main.cpp:1344), plus the end-to-end host-API time of the same decode
-    (LR table / host exp + PCIe + decode + copy back) -- the in-process
-    replacement of decoder.py's 272 ldpc.exe runs (decoder.py:553-562)."""
+    reads) at the pipeline's max_iter, device-resident (the count differences
+    k as int8 codes with the table k * ln49, LR = host libm exp as
+    DNA_main.cpp:1344; --input fp64: fp64 LR), plus the end-to-end host-API
+    time of the same decode (code table / host exp + PCIe + decode + copy
+    back) -- the in-process replacement of decoder.py's 272 ldpc.exe runs
+    (decoder.py:553-562)."""
     import ldpc_amd as L
     import synth
     cw = synth.load_codewords()
@@ -296,12 +298,22 @@ def dna272(args, og, threads, max_iter=200):
     G = L.Graph(synth.PCHK)
     B, N = llr.shape
     eng = L.Engine(G, 0, "bp", chunk=B)
-    d_in = L.DeviceBuffer(0, B * N * 8)
-    d_in.upload(np.ascontiguousarray(lr))
     d_h, d_i, d_v = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
+    k = np.rint(llr / synth.LLR_UNIT)
+    if args.input == "code" and np.array_equal(k * synth.LLR_UNIT, llr) and np.abs(k).max() <= 127:
+        d_in = L.DeviceBuffer(0, B * N)
+        d_in.upload(np.ascontiguousarray(k.astype(np.int8)))
+        table = np.arange(-128, 128, dtype=np.float64) * synth.LLR_UNIT
 
-    def step():
-        eng.decode(d_in.at(0), L.IN_LR, B, max_iter, d_h.at(0), None, L.POST_LLR, d_i.at(0), d_v.at(0))
+        def step():
+            eng.decode_codes(d_in.at(0), table, L.IN_LLR, B, max_iter, d_h.at(0), None, L.POST_LLR, d_i.at(0),
+                             d_v.at(0))
+    else:
+        d_in = L.DeviceBuffer(0, B * N * 8)
+        d_in.upload(np.ascontiguousarray(lr))
+
+        def step():
+            eng.decode(d_in.at(0), L.IN_LR, B, max_iter, d_h.at(0), None, L.POST_LLR, d_i.at(0), d_v.at(0))
 
     for _ in range(max(1, args.warmup)):
         step()
@@ -322,14 +334,14 @@ def dna272(args, og, threads, max_iter=200):
         h2, _, it2, v2 = G.decode(llr, max_iter=max_iter, post=None)
         th.append(time.perf_counter() - t)
     assert np.array_equal(h2, hard) and np.array_equal(it2, it)
-    out = {"workload": f"dna272-bp{max_iter}", "batch": B, "max_iter": max_iter,
+    out = {"workload": f"dna272-bp{max_iter}", "batch": B, "max_iter": max_iter, "input": args.input,
            "value": round(B / el, 1), "unit": "codewords/s", "ms_per_decode_device": round(el * 1e3, 3),
            "mean_iters": round(float(it.mean()), 3), "genie_ok": int((hard == cw).all(axis=1).sum()),
            "host_api_ms_median": round(float(np.median(th)) * 1e3, 3),
            "host_api_ms_min": round(float(np.min(th)) * 1e3, 3),
            "host_api_calls": len(th),
-           "host_api_includes": "ldpc_decode end to end: host LR (exp table for the k*ln49 alphabet, else host exp) "
-                                "+ H2D + decode + packed hard-bit D2H + unpack"}
+           "host_api_includes": "ldpc_decode end to end: host encode of the k*ln49 alphabet to int8 codes (else host "
+                                "exp) + H2D + decode + packed hard-bit D2H + unpack"}
     if og is not None:
         t = time.perf_counter()
         rh, _, rit, rv = og.decode_batch(llr, max_iter, threads=threads, want_post=False)
