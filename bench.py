@@ -375,6 +375,43 @@ def channel(L, eng, args, dev, N, b0, B, d_cw, n_cw, p, kind):
     return d_in, decode
 
 
+def fp64_leg(args, L, eng, G, dev, b0, B, d_cw, n_cw, in_kind, iters, valid, d_hard):
+    """The headline workload with the channel output as fp64 values in HBM
+    (--input fp64) on the same engine: 1 warm-up + 2 timed decodes, and the
+    proof that it is the same decode -- iteration counts and valid flags of
+    every codeword and the hard bits of 1024 codewords spread over the shard
+    equal the coded headline's."""
+    N = G.N
+    args_fp = argparse.Namespace(**{**vars(args), "input": "fp64"})
+    d_in, decode = channel(L, eng, args_fp, dev, N, b0, B, d_cw, n_cw, args.p, in_kind)
+    dh, di, dv = L.DeviceBuffer(dev, B * N), L.DeviceBuffer(dev, B * 4), L.DeviceBuffer(dev, B)
+    decode(B, args.max_iter, dh.at(0), di.at(0), dv.at(0))
+    eng.sync()
+    eng.profile(0 if args.no_profile else 64)
+    steps = 2
+    t = time.perf_counter()
+    for _ in range(steps):
+        decode(B, args.max_iter, dh.at(0), di.at(0), dv.at(0))
+    eng.sync()
+    el = time.perf_counter() - t
+    st = eng.stats()
+    it2 = di.download(np.empty(B, np.int32))
+    v2 = dv.download(np.empty(B, np.uint8))
+    rows = np.unique(np.linspace(0, B - 1, min(B, 1024)).astype(np.int64))
+    same_hard = all(np.array_equal(dh.download(np.empty(N, np.uint8), offset=int(r) * N),
+                                   d_hard.download(np.empty(N, np.uint8), offset=int(r) * N)) for r in rows)
+    same = bool(np.array_equal(it2, iters) and np.array_equal(v2, valid) and same_hard)
+    avg = {k: round(v["ms"] / v["sampled"], 4) if v["sampled"] else 0.0 for k, v in st.items()}
+    for b in (d_in, dh, di, dv):
+        b.free()
+    return {"input": "fp64 LR in HBM (LR = host exp(+-ln49))", "batch": B, "steps": steps,
+            "value": round(B * steps / el, 1), "unit": "codewords/s", "ms_per_step": round(el / steps * 1e3, 2),
+            "avg_ms": avg, "kernels": kernel_names(eng, "bp", False),
+            "same_as_coded": same, "compared": f"iterations + valid flags of all {B}, hard bits of {len(rows)} codewords",
+            "check": {"checked": len(rows), "mismatches": 0 if same else 1,
+                      "what": "the fp64-input decode vs the coded headline decode (bit-identical)"}}
+
+
 def msa_1m(args, og, threads, cw, d_cw):
     """Config 5: min-sum (Run_MSA_Decoder_INF) with early termination on
     `--msa-batch` codewords of BSC(p = 0.002), 1 warm-up + 2 timed decodes,
@@ -564,12 +601,17 @@ def main():
                             "a sample of every rank's own shard (N = 1: the cpu_baseline sample)"}
     mismatches = out["check"]["mismatches"]
 
-    # ---- secondary legs (N = 1): config 2 and config 5, each checked ----
+    # ---- secondary legs (N = 1): config 3 on fp64 input, config 5 and config 2, each checked ----
     if world == 1 and args.secondary and args.global_batch == 0 and algo == "bp":
+        sec = {"note": "driver-timed after the headline region; not part of value / ms_per_step"}
+        if args.input == "code":
+            t = time.perf_counter()
+            sec["config3_fp64_input"] = fp64_leg(args, L, eng, G, dev, b0, B, d_cw, cw.shape[0], in_kind, iters, valid,
+                                                 d_hard)
+            sec["config3_fp64_input"]["leg_wall_s"] = round(time.perf_counter() - t, 2)
         for b in (d_in, d_hard, d_iters, d_valid):
             b.free()
         eng.close()
-        sec = {"note": "driver-timed after the headline region; not part of value / ms_per_step"}
         t = time.perf_counter()
         sec["config5_msa_1m"] = msa_1m(args, og, cpus["effective"], cw, d_cw)
         sec["config5_msa_1m"]["leg_wall_s"] = round(time.perf_counter() - t, 2)

@@ -149,3 +149,34 @@ def test_changing_tables_between_decodes(gpu, codewords):
     ref = G2.decode(k.astype(np.float64) * 0.7, max_iter=30, post="ratio", schedule=dict(lr_table=False))
     assert np.array_equal(outs[1][0], ref[0]) and np.array_equal(outs[1][2], ref[2])
     assert np.array_equal(outs[1][1].view(np.uint64), ref[1].view(np.uint64))
+
+
+@pytest.mark.parametrize("algo", ["bp", "msa"])
+def test_coded_nonfinite_table_entries(gpu, G, codewords, algo):
+    """Table entries NaN / +-inf / -0.0 (the NaN guards of dec.cpp:676-687 and
+    the min-sum sign / NaN rules): the coded decode equals the fp64 decode of
+    table[code + 128] bit for bit, posterior NaN positions included."""
+    L = gpu
+    N = G.N
+    rng = np.random.default_rng(5)
+    k = rng.integers(-3, 4, size=(130, N)).astype(np.int8)
+    k[rng.random(k.shape) < 0.6] = 1  # mostly a confident 0
+    table = _table()
+    table[128 + 2] = np.nan
+    table[128 - 3] = -np.inf
+    table[128 + 3] = np.inf
+    table[128] = -0.0
+    bp = algo == "bp"
+    vals = table[k.astype(np.int64) + 128]
+    B = len(k)
+    codes = L.DeviceBuffer(0, B * N)
+    codes.upload(k)
+    fp = L.DeviceBuffer(0, B * N * 8)
+    with np.errstate(over="ignore", invalid="ignore"):
+        fp.upload(np.ascontiguousarray(np.exp(vals) if bp else vals))
+    eng = L.Engine(G, 0, algo)
+    kind = L.IN_LR if bp else L.IN_LLR
+    post = L.POST_RATIO if bp else L.POST_LLR
+    a = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode_codes(codes.at(0), table, L.IN_LLR, B, 20, h, pp, post, it, v))
+    b = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode(fp.at(0), kind, B, 20, h, pp, post, it, v))
+    _same(a, b)
