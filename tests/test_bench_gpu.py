@@ -54,6 +54,11 @@ def test_bench_secondary_legs(gpu):
     d = sec["config2_dna272"]
     assert d["genie_ok"] == 272 and d["check"]["mismatches"] == 0 and d["check"]["checked"] == 272
     assert d["host_api_ms_median"] > 0
+    # the headline on fp64 input decodes exactly what the coded headline does
+    f = sec["config3_fp64_input"]
+    assert f["same_as_coded"] and f["value"] > 0 and f["batch"] == 1024
+    assert out["config"]["input"].startswith("int8") and "true>" in out["roofline"]["kernels"]["variable"]
+    assert "false>" in f["kernels"]["variable"]
 
 
 def test_bench_dna272_line(gpu):
