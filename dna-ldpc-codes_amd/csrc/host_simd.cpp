@@ -19,7 +19,10 @@ __attribute__((target_clones("avx2", "default"))) bool host_encode_lattice(const
     for (size_t i = i0; i < i1; i++) {
         const double x = src[i];
         const double kd = (x * inv + magic) - magic;
-        bad |= (int)(kd * unit != x) | (int)!(kd <= lim && kd >= -lim);
+        // -0.0 compares equal to 0 * unit but is not its bits (min-sum sums
+        // keep the sign of a zero): off the lattice
+        bad |= (int)(kd * unit != x) | (int)!(kd <= lim && kd >= -lim) |
+               (int)(__builtin_bit_cast(unsigned long long, x) == 0x8000000000000000ull);
         // clamp with plain compares (vectorise to blends; fmin / fmax would be
         // library calls here): NaN becomes -lim, and such a value is flagged bad
         double kc = kd >= -lim ? kd : -lim;

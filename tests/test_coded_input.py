@@ -180,3 +180,22 @@ def test_coded_nonfinite_table_entries(gpu, G, codewords, algo):
     a = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode_codes(codes.at(0), table, L.IN_LLR, B, 20, h, pp, post, it, v))
     b = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode(fp.at(0), kind, B, 20, h, pp, post, it, v))
     _same(a, b)
+
+
+@pytest.mark.parametrize("algo", ["bp", "msa"])
+def test_host_api_negative_zero_and_off_lattice(G, og, codewords, algo):
+    """ldpc_decode's code table path takes only exact lattice batches: a -0.0
+    LLR (equal to 0 * unit, other bits; min-sum sums keep a zero's sign) or an
+    off-lattice value sends the batch through the fp64 path; results equal the
+    oracle bit for bit, posterior included."""
+    a = 0 if algo == "bp" else 1
+    llr = synth.dna_like_llrs(codewords, seed=12, reads=57000)[:96].copy()
+    zeros = np.argwhere(llr == 0)
+    assert len(zeros) > 10
+    r, c = zeros[:10].T
+    llr[r, c] = -0.0
+    for case in (llr, np.where(np.arange(llr.shape[1]) == 7, llr * 1.0000001, llr)):
+        ref_h, ref_p, ref_it, ref_v = og.decode_batch(case, 40, algo=a, post_mode=1 if a == 0 else 0, threads=8)
+        h, p, it, v = G.decode(case, max_iter=40, algo=algo, post="ratio" if a == 0 else "llr")
+        assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
+        assert np.array_equal(p.view(np.uint64), ref_p.view(np.uint64))
