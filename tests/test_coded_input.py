@@ -194,8 +194,9 @@ def test_host_api_negative_zero_and_off_lattice(G, og, codewords, algo):
     assert len(zeros) > 10
     r, c = zeros[:10].T
     llr[r, c] = -0.0
-    for case in (llr, np.where(np.arange(llr.shape[1]) == 7, llr * 1.0000001, llr)):
-        ref_h, ref_p, ref_it, ref_v = og.decode_batch(case, 40, algo=a, post_mode=1 if a == 0 else 0, threads=8)
-        h, p, it, v = G.decode(case, max_iter=40, algo=algo, post="ratio" if a == 0 else "llr")
+    # max_iter 0: the posterior is the input itself (a -0.0 must come back as -0.0)
+    for case, mi in ((llr, 0), (llr, 40), (np.where(np.arange(llr.shape[1]) == 7, llr * 1.0000001, llr), 40)):
+        ref_h, ref_p, ref_it, ref_v = og.decode_batch(case, mi, algo=a, post_mode=1 if a == 0 else 0, threads=8)
+        h, p, it, v = G.decode(case, max_iter=mi, algo=algo, post="ratio" if a == 0 else "llr")
         assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
         assert np.array_equal(p.view(np.uint64), ref_p.view(np.uint64))
