@@ -53,7 +53,10 @@ sys.path[:0] = [os.path.join(ROOT, "dna-ldpc-codes_amd")]
 
 METRIC = "decoded codewords/sec (n=18432, m=2048, 50 BP iters) at 1/2/4/8 GPUs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
-VAR_CPW = 4  # the engine's default columns per variable-phase wave (kernel instantiation names)
+# the engine's default columns per variable-phase wave (kernel instantiation
+# names): 2 with coded priors in the resident pool or the compressed min-sum,
+# else 4 (engine.hip var_cpw_for)
+VAR_CPW, VAR_CPW_CODED = 4, 2
 
 
 def parse():
@@ -167,16 +170,17 @@ def kernel_names(eng, algo, coded=False) -> dict:
     PC, coded priors (coded input on a continuous schedule)."""
     msa = "true" if algo == "msa" else "false"
     pc = str(bool(coded) and eng.continuous).lower()
+    cpw = VAR_CPW_CODED if pc == "true" and (eng.resident or eng.msa_compressed) else VAR_CPW
     if eng.msa_compressed:
         nt = str(eng.nontemporal).lower()
         return {"check": f"k_check_msa_c<72,{nt}>",
-                "variable": f"k_var_msa_c<72,8,{str(eng.continuous).lower()},{VAR_CPW},{nt},{pc}>"}
+                "variable": f"k_var_msa_c<72,8,{str(eng.continuous).lower()},{cpw},{nt},{pc}>"}
     chk = "k_check_msa" if algo == "msa" else "k_check_bp"
     if eng.resident:
-        return {"check": f"{chk}<72,false,true>", "variable": f"k_var_m<{msa},8,false,true,{VAR_CPW},true,{pc}>"}
+        return {"check": f"{chk}<72,false,true>", "variable": f"k_var_m<{msa},8,false,true,{cpw},true,{pc}>"}
     nt = str(eng.nontemporal).lower()
     return {"check": f"{chk}<72,{nt},false>",
-            "variable": f"k_var_m<{msa},8,{nt},{str(eng.continuous).lower()},{VAR_CPW},false,{pc}>"}
+            "variable": f"k_var_m<{msa},8,{nt},{str(eng.continuous).lower()},{cpw},false,{pc}>"}
 
 
 def algorithmic_bytes(eng, N, M, E) -> dict:

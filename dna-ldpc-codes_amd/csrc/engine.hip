@@ -42,7 +42,9 @@ namespace ldpc {
 // Defaults, each chosen by a same-process A/B on MI355X.
 constexpr int32_t kDefaultGroupTiles = 3;     // grouped schedule (tools/sweep.py)
 constexpr int32_t kDefaultMsaGroupTiles = 4;  // compressed min-sum, 1024-lane pool
-constexpr int32_t kDefaultVarCpw = 4;         // +2.6-2.9 % over 1 column per wave
+constexpr int32_t kDefaultVarCpw = 4;         // fp64 priors: +2.6-2.9 % over 1 column per wave
+constexpr int32_t kDefaultVarCpwCoded = 2;    // coded priors, resident pool / compressed min-sum: +0.5 % / +1.9 %
+                                              // over 4 (the grouped BP schedule stays at 4: 2 is 10 % slower)
 constexpr int32_t kDefaultPoolTiles = 3;      // resident pool: 3 x 85 MB ~ the 256 MB Infinity Cache
 constexpr int32_t kDefaultResPoll = 8;
 constexpr int32_t kDefaultSynBlocks = 32;     // continuous-mode syndrome blocks per tile (config 5 +5-6 %)
@@ -67,8 +69,9 @@ ldpc_schedule resolve_schedule(const ldpc_schedule* s)
     r.flags &= kAllFlags;
     r.flags_set = kAllFlags | kResolved | ((r.flags_set & LDPC_SCHED_RESIDENT) ? kResChosen : 0);
     if (r.group_tiles == 0) r.group_tiles = -2;  // per-algorithm default, resolved at init
-    // (3: compressed min-sum only; the fp64 variable kernels take 1, 2, 4 or 8)
-    if (r.var_cpw < 1 || r.var_cpw > 8 || (r.var_cpw > 4 && r.var_cpw != 8)) r.var_cpw = kDefaultVarCpw;
+    // (3: compressed min-sum only; the fp64 variable kernels take 1, 2, 4 or
+    // 8); -2: the default, chosen per decode by the prior's form (var_cpw_for)
+    if (r.var_cpw < 1 || r.var_cpw > 8 || (r.var_cpw > 4 && r.var_cpw != 8)) r.var_cpw = -2;
     if (r.pool_tiles <= 0) r.pool_tiles = kDefaultPoolTiles;
     if (r.poll_every <= 0) r.poll_every = kDefaultResPoll;
     if (r.syn_blocks <= 0) r.syn_blocks = kDefaultSynBlocks;
@@ -493,6 +496,15 @@ static void var_m(bool nt, bool cont, bool inplace, int cpw, hipStream_t s, dim3
     else var_m_cpw<MSA, false, false, false>(cpw, s, grid, c2v, v2c, prior, hard, active, col_edge, pt, N, E, t0, rf);
 }
 
+// columns per variable-phase wave: the schedule's, or by default 2 for coded
+// priors in the resident pool and the compressed min-sum, else 4 (same-box
+// A/Bs, profiles/r3/coded/cpw_probe.txt)
+int Engine::var_cpw_for(const dev::Refill& rf) const
+{
+    if (var_cpw > 0) return var_cpw;
+    return (rf.fresh && rf.in_code && (res || msa_c)) ? kDefaultVarCpwCoded : kDefaultVarCpw;
+}
+
 // variable phase (+ hard decisions, optional posterior, continuous mode's
 // refills and finished lanes' outputs) of tiles t0 .. t0+gt-1
 int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt, const dev::Refill& rf)
@@ -503,7 +515,7 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
     const bool reg8 = g->regular_dv && g->dv_max == 8;
     const bool cnt = rf.fresh != nullptr;
     if (msa_c) {  // N % 16 == 0 (init)
-        int cpw = var_cpw >= 4 ? 4 : var_cpw;
+        int cpw = std::min(var_cpw_for(rf), 4);
         if (N % (4 * cpw) != 0) cpw = 1;  // (N % 16 == 0: every CPW but 3 divides)
         const unsigned nb = gt * (unsigned)(N / (4 * cpw));
         const double* rec = msa_rec(scratch);
@@ -538,7 +550,8 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
     }
     if (reg8) {
         const bool inplace = scratch == v2c;
-        const int cpw = (var_cpw != 3 && N % (4 * var_cpw) == 0) ? var_cpw : 1;
+        const int want = var_cpw_for(rf);
+        const int cpw = (want != 3 && N % (4 * want) == 0) ? want : 1;
         const dim3 grid((unsigned)((N + 4 * cpw - 1) / (4 * cpw)), gt);
         LAUNCH_ON(s, K_VAR, {
             if (algo == LDPC_ALGO_MSA) var_m<true>(nt_d, cnt, inplace, cpw, s, grid, scratch, v2c, prior, hard, active, d_col_edge, pt, N, E, t0, rf);

@@ -52,7 +52,7 @@ struct Engine {
     bool res = false;         // resident pool: a few tiles iterated in place, syndrome in the check kernel
     bool first_fp = false;    // single-fill BP: the first check reads the prior (k_check_bp_first)
     bool debug_no_drain = false;  // LDPC_SCHED_DEBUG_NO_DRAIN: the host ignores a drained pool
-    int var_cpw = 4;          // variable phase: columns per wave
+    int var_cpw = 4;          // variable phase: columns per wave (-2: by the prior's form, var_cpw_for)
     int res_poll = 8;         // res: steps between occupancy polls
     int syn_blocks = 0;       // continuous grouped mode: k_syndrome_split blocks per tile
     uint8_t* d_sgn = nullptr; // msa_c: [tile][N][64] sign bits of the v2c each column last stored
@@ -153,6 +153,7 @@ struct Engine {
     int probe(int probes);
     int launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt);
     int launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, double* pt, const dev::Refill& rf);
+    int var_cpw_for(const dev::Refill& rf) const;
 };
 
 // bytes of device memory per resident codeword

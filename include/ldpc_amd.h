@@ -106,7 +106,9 @@ typedef struct ldpc_schedule {
     int32_t flags;
     int32_t group_tiles; /* grouped schedule: 64-codeword tiles per check/variable launch
                             (0 = default: 3, 4 for compressed min-sum; < 0 = the whole pass) */
-    int32_t var_cpw;     /* columns per variable-phase wavefront: 1, 2, 4 or 8 (0 = default 4) */
+    int32_t var_cpw;     /* columns per variable-phase wavefront: 1, 2, 4 or 8 (3: compressed min-sum only;
+                            0 = default: 2 for coded input in the resident pool or the compressed
+                            min-sum, else 4) */
     int32_t pool_tiles;  /* resident pool tiles when the engine chooses the pool (0 = default 3) */
     int32_t poll_every;  /* resident pool: steps between occupancy polls (0 = default 8) */
     int32_t syn_blocks;  /* continuous grouped schedule: syndrome blocks per tile (0 = default 32) */

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--chunk", type=int, default=16384)
     ap.add_argument("--profile", type=int, default=0, help="HIP-event sample stride per kernel class (0: off)")
+    ap.add_argument("--input", default="fp64", choices=["fp64", "code"],
+                    help="channel output as fp64 LLRs or int8 codes + table (ldpc_engine_decode_codes)")
     ap.add_argument("--fresh", type=int, default=0,
                     help="rounds of create/time/free per variant (averages allocation placement); 0 = one "
                          "engine per variant, timed --reps times")
@@ -42,7 +44,22 @@ def main():
     B, N = args.batch, G.N
     d_cw = L.DeviceBuffer(0, cw.size)
     d_cw.upload(np.ascontiguousarray(cw))
-    d_in = L.DeviceBuffer(0, B * N * 8)
+    coded = args.input == "code"
+    d_in = L.DeviceBuffer(0, B * N * (1 if coded else 8))
+    table = np.arange(-128, 128, dtype=np.float64) * synth.LLR_UNIT
+
+    def gen(e):
+        if coded:
+            e.gen_bsc_codes(d_in.at(0), 0, B, d_cw.at(0), cw.shape[0], 2026, args.p)
+        else:
+            e.gen_bsc(d_in.at(0), L.IN_LLR, 0, B, d_cw.at(0), cw.shape[0], 2026, args.p, synth.LLR_UNIT)
+
+    def run(e):
+        if coded:
+            e.decode_codes(d_in.at(0), table, L.IN_LLR, B, args.max_iter, d_h.at(0), None, L.POST_LLR, d_i.at(0),
+                           d_v.at(0))
+        else:
+            e.decode(d_in.at(0), L.IN_LLR, B, args.max_iter, d_h.at(0), None, L.POST_LLR, d_i.at(0), d_v.at(0))
     d_h, d_i, d_v = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
     def make(spec):
         name, _, kvs = spec.partition(":")
@@ -64,13 +81,12 @@ def main():
             for spec in args.var[k0:] + args.var[:k0]:
                 name, e = make(spec)
                 if gen is None:
-                    e.gen_bsc(d_in.at(0), L.IN_LLR, 0, B, d_cw.at(0), cw.shape[0], 2026, args.p, synth.LLR_UNIT)
+                    gen(e)
                     gen = True
                 ts = []
                 for k in range(2):  # warm-up + timed
                     t = time.perf_counter()
-                    e.decode(d_in.at(0), L.IN_LLR, B, args.max_iter, d_h.at(0), None, L.POST_LLR, d_i.at(0),
-                             d_v.at(0))
+                    run(e)
                     e.sync()
                     ts.append(time.perf_counter() - t)
                 it = d_i.download(np.empty(B, np.int32))
@@ -93,14 +109,14 @@ def main():
         if args.profile:
             e.profile(args.profile)
         engines.append((name, e))
-    engines[0][1].gen_bsc(d_in.at(0), L.IN_LLR, 0, B, d_cw.at(0), cw.shape[0], 2026, args.p, synth.LLR_UNIT)
+    gen(engines[0][1])
     engines[0][1].sync()
     times = {n: [] for n, _ in engines}
     ref = None
     for rep in range(args.reps + 1):
         for name, e in engines:
             t = time.perf_counter()
-            e.decode(d_in.at(0), L.IN_LLR, B, args.max_iter, d_h.at(0), None, L.POST_LLR, d_i.at(0), d_v.at(0))
+            run(e)
             e.sync()
             el = time.perf_counter() - t
             if rep > 0:
