@@ -163,14 +163,17 @@ def cpu_baseline(args, og, llr_fn, B, gpu_out, cpus):
     return cb, (c0 + c1, bad0 + bad1)
 
 
-def kernel_names(eng, algo, coded=False) -> dict:
+def kernel_names(eng, algo, coded=False, cpw=None) -> dict:
     """Template instantiations of the check / variable kernels an engine
     launches (csrc/engine.hip launch_check / launch_var), as rocprofv3 names
     them (tools/pmc_r3.py short form); the variable kernels' last argument is
     PC, coded priors (coded input on a continuous schedule)."""
     msa = "true" if algo == "msa" else "false"
     pc = str(bool(coded) and eng.continuous).lower()
-    cpw = VAR_CPW_CODED if pc == "true" and (eng.resident or eng.msa_compressed) else VAR_CPW
+    if not cpw:  # the engine's default (an explicit --var-cpw names itself)
+        cpw = VAR_CPW_CODED if pc == "true" and (eng.resident or eng.msa_compressed) else VAR_CPW
+    elif eng.msa_compressed:
+        cpw = min(cpw, 4)
     if eng.msa_compressed:
         nt = str(eng.nontemporal).lower()
         return {"check": f"k_check_msa_c<72,{nt}>",
@@ -234,12 +237,12 @@ def find_traffic(kname):
     return None, None
 
 
-def roofline(eng, G, st, cw_iters, coded=False) -> dict:
+def roofline(eng, G, st, cw_iters, coded=False, cpw=None) -> dict:
     """Roofline of the dominant kernel: algorithmic bytes per launch / its
     average launch duration (HIP events on the kernel's dispatch packet)."""
     N, M, E = G.N, G.M, G.E
     by_kernel = algorithmic_bytes(eng, N, M, E)
-    names = kernel_names(eng, "msa" if eng.algo == 1 else "bp", coded)
+    names = kernel_names(eng, "msa" if eng.algo == 1 else "bp", coded, cpw)
 
     def avg_ms(k):
         return st[k]["ms"] / st[k]["sampled"] if st[k]["sampled"] else 0.0
@@ -410,7 +413,7 @@ def fp64_leg(args, L, eng, G, dev, b0, B, d_cw, n_cw, in_kind, iters, valid, d_h
         b.free()
     return {"input": "fp64 LR in HBM (LR = host exp(+-ln49))", "batch": B, "steps": steps,
             "value": round(B * steps / el, 1), "unit": "codewords/s", "ms_per_step": round(el / steps * 1e3, 2),
-            "avg_ms": avg, "kernels": kernel_names(eng, "bp", False),
+            "avg_ms": avg, "kernels": kernel_names(eng, "bp", False, args.var_cpw or None),
             "same_as_coded": same, "compared": f"iterations + valid flags of all {B}, hard bits of {len(rows)} codewords",
             "check": {"checked": len(rows), "mismatches": 0 if same else 1,
                       "what": "the fp64-input decode vs the coded headline decode (bit-identical)"}}
@@ -576,7 +579,7 @@ def main():
                    "continuous": eng.continuous, "resident_pool": eng.resident,
                    "compressed_msa": eng.msa_compressed, "syndrome_split": eng.syndrome_split,
                    "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 4)},
-        "roofline": roofline(eng, G, st, cw_iters, args.input == "code"),
+        "roofline": roofline(eng, G, st, cw_iters, args.input == "code", args.var_cpw or None),
     }
 
     # ---- correctness of the timed decode: every rank checks its own shard ----
