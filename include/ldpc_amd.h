@@ -94,9 +94,10 @@ enum {
                                            spread over syn_blocks blocks per tile */
     LDPC_SCHED_FIRST_FROM_PRIOR = 1 << 12, /* single-fill BP decodes: the first check derives its messages
                                               from the prior instead of E stored copies (default on) */
-    LDPC_SCHED_LR_TABLE = 1 << 13,      /* ldpc_decode, BP with host exp: LLR batches on a k * unit lattice
-                                           cross PCIe as one byte each + a table of host exp(k * unit)
-                                           (default on; off = host exp of every value) */
+    LDPC_SCHED_LR_TABLE = 1 << 13,      /* ldpc_decode, BP (host exp) and min-sum: LLR batches on a k * unit
+                                           lattice cross PCIe as one byte each and are decoded as codes with the
+                                           table k * unit (BP: its host exp), as ldpc_engine_decode_codes
+                                           (default on; off = fp64 input: host exp / copy of every value) */
     LDPC_SCHED_DEBUG_NO_DRAIN = 1 << 14 /* tests only: the host ignores a drained pool, so a decode runs
                                            into its step bound and returns LDPC_ERR_DEVICE (default off) */
 };
