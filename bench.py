@@ -3,6 +3,7 @@
 iterations (BASELINE.json metric), one process per GPU.
 
     python bench.py                       # N=1, 100k synthetic codewords per step
+    python bench.py --gpus N              # N ranks: starts torch.distributed.run as a child
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Workload (SURVEY 8(d) config 3, weak-scaled per GPU by default): every
@@ -25,11 +26,12 @@ times and a gather of their check counts (gloo, CPU tensors).  `value` = all
 codewords of all ranks / max elapsed.
 
 Correctness of the timed decode, on every rank: the oracle decodes a sample of
-the rank's own shard (at N = 1 the cpu_baseline leg's sample, at N > 1 about
-16 codewords per host thread of the rank's share of the cores, from both ends
-of the shard) and its hard bits, iteration counts and valid flags must equal
-the GPU's; `check` in the JSON line carries the per-rank counts and any
-mismatch exits non-zero.
+the rank's own shard -- its head (at N = 1 the cpu_baseline leg's sample, at
+N > 1 about 8 codewords per host thread of the rank's share of the cores), its
+last rows (the lane pool's drain) and 32 random interior rows -- and its hard
+bits, iteration counts and valid flags must equal the GPU's; `check` in the
+JSON line carries the per-rank counts and rows, and any mismatch exits
+non-zero.
 
 At N = 1 (unless --secondary 0) two driver-timed secondary legs follow the
 headline, each with its own oracle check, under "secondary": config 2 (the
@@ -81,7 +83,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--check-per-thread", type=int, default=16,
                     help="N > 1 (and --cpu-baseline 0): oracle-checked codewords per host thread of each rank")
-    ap.add_argument("--group-tiles", type=int, default=-1, help="tiles per check/variable launch (-1: engine default)")
+    ap.add_argument("--group-tiles", type=int, default=None,
+                    help="tiles per check/variable launch (unset or 0: engine default; < 0: the whole pass, as the ABI)")
     ap.add_argument("--nt", type=int, default=-1, help="nontemporal d-stream (-1: engine default)")
     ap.add_argument("--cont", type=int, default=-1, help="continuous batching / lane refill (-1: engine default)")
     ap.add_argument("--res", type=int, default=-1,
@@ -122,22 +125,45 @@ def _oracle():
 
 
 def oracle_check(og, llr_fn, gpu_out, algo, max_iter, ranges, threads):
-    """Oracle vs GPU on shard rows `ranges` [(start, n)]: (checked, mismatching
-    rows, oracle seconds, oracle codewords)."""
+    """Oracle vs GPU on shard rows `ranges`: (start, n) runs and / or arrays of
+    row indices.  Returns (checked, mismatching rows, oracle seconds)."""
     checked, bad, el = 0, [], 0.0
-    for start, n in ranges:
-        if n <= 0:
-            continue
-        llr = llr_fn(start, n)
+    for rg in ranges:
+        if isinstance(rg, tuple):
+            start, n = rg
+            if n <= 0:
+                continue
+            rows = np.arange(start, start + n)
+            llr = llr_fn(start, n)
+            h, it, v = gpu_out(start, n)
+        else:
+            rows = np.asarray(rg, dtype=np.int64)
+            if rows.size == 0:
+                continue
+            llr = np.concatenate([llr_fn(int(r), 1) for r in rows])
+            outs = [gpu_out(int(r), 1) for r in rows]
+            h = np.concatenate([o[0] for o in outs])
+            it = np.concatenate([np.asarray(o[1]) for o in outs])
+            v = np.concatenate([np.asarray(o[2]) for o in outs])
         t = time.perf_counter()
         rh, _, rit, rv = og.decode_batch(llr, max_iter, algo=algo, threads=threads, want_post=False)
         el += time.perf_counter() - t
-        h, it, v = gpu_out(start, n)
-        for k in range(n):
+        for k, r in enumerate(rows):
             if not (np.array_equal(h[k], rh[k]) and it[k] == rit[k] and bool(v[k]) == bool(rv[k])):
-                bad.append(start + k)
-        checked += n
+                bad.append(int(r))
+        checked += len(rows)
     return checked, bad, el
+
+
+def tail_and_interior(B, lo, n_tail=32, n_interior=32, seed=0):
+    """Rows of a shard [0, B) outside a checked head [0, lo): its last n_tail
+    rows (the lane pool's drain) and n_interior random rows in between."""
+    t0 = max(lo, B - n_tail)
+    tail = np.arange(t0, B, dtype=np.int64)
+    pool = np.arange(lo, t0, dtype=np.int64)
+    interior = np.sort(np.random.default_rng(seed).choice(pool, min(n_interior, pool.size), replace=False)) \
+        if pool.size else pool
+    return tail, interior
 
 
 def cpu_baseline(args, og, llr_fn, B, gpu_out, cpus):
@@ -153,6 +179,10 @@ def cpu_baseline(args, og, llr_fn, B, gpu_out, cpus):
     n = max(1, min(threads * rounds, B - n0))
     start = n0 if B > n0 else 0
     c1, bad1, el = oracle_check(og, llr_fn, gpu_out, algo, args.max_iter, [(start, n)], threads)
+    # beyond the timed sample: the shard's drain (last rows) and its interior
+    tail, inter = tail_and_interior(B, start + n, seed=args.seed)
+    c2, bad2, _ = oracle_check(og, llr_fn, gpu_out, algo, args.max_iter, [tail, inter], threads)
+    rows = {"head": [0, start + n], "tail": [int(tail[0]), B] if tail.size else None, "interior": inter.tolist()}
     cb = {"value": round(n / el, 3), "unit": "codewords/s", "cores": threads, "kind": "port",
           "per_core": round(n / el / threads, 3),
           "host": cpus,
@@ -160,7 +190,7 @@ def cpu_baseline(args, og, llr_fn, B, gpu_out, cpus):
                     f"{args.max_iter} iters, oracle/ldpc_oracle.c on {threads} host threads: every CPU this process "
                     f"may use (the affinity mask lists {cpus['affinity']}, the cgroup CPU quota allows "
                     f"{cpus['cgroup_quota_cpus']}; more threads than the quota only time-slice it), {el:.1f} s"}
-    return cb, (c0 + c1, bad0 + bad1)
+    return cb, (c0 + c1 + c2, bad0 + bad1 + bad2, rows)
 
 
 def kernel_names(eng, algo, coded=False, cpw=None) -> dict:
@@ -204,10 +234,21 @@ def algorithmic_bytes(eng, N, M, E) -> dict:
     }
 
 
+def moved_bytes(eng, N, M, E, coded=False) -> dict:
+    """Bytes each kernel moves per executed codeword-iteration: the
+    algorithmic bytes, with the prior read as its 1-byte code instead of an
+    fp64 value where the continuous schedules keep coded priors (DESIGN.md
+    sec. 4.3)."""
+    b = dict(algorithmic_bytes(eng, N, M, E))
+    if coded and eng.continuous:
+        b["variable"] -= 7.0 * N
+    return b
+
+
 def bound_detail(eng, coded=False) -> str:
     note = (" Coded input: the variable kernel reads each column's prior as a 1-byte code (+ a 2 KB table), "
             "7 B per column and codeword-iteration fewer than the algorithmic (fp64 prior) bytes that `achieved` "
-            "counts." if coded and eng.continuous else "")
+            "counts; `achieved_moved` counts the code." if coded and eng.continuous else "")
     return _bound_detail(eng) + note
 
 
@@ -242,6 +283,7 @@ def roofline(eng, G, st, cw_iters, coded=False, cpw=None) -> dict:
     average launch duration (HIP events on the kernel's dispatch packet)."""
     N, M, E = G.N, G.M, G.E
     by_kernel = algorithmic_bytes(eng, N, M, E)
+    moved = moved_bytes(eng, N, M, E, coded)
     names = kernel_names(eng, "msa" if eng.algo == 1 else "bp", coded, cpw)
 
     def avg_ms(k):
@@ -252,8 +294,11 @@ def roofline(eng, G, st, cw_iters, coded=False, cpw=None) -> dict:
     k_avg = avg_ms(dom)
     bytes_per_launch = by_kernel[dom] * cw_iters / k_launch
     achieved = bytes_per_launch / (k_avg * 1e-3) / 1e9 if k_avg > 0 else None
+    moved_per_launch = moved[dom] * cw_iters / k_launch
+    achieved_moved = moved_per_launch / (k_avg * 1e-3) / 1e9 if k_avg > 0 else None
     it_ms = sum(avg_ms(k) * st[k]["launches"] for k in ("check", "variable", "syndrome"))
-    iter_bytes = (32.0 * E + 10.0 * N) * cw_iters
+    iter_bytes = (32.0 * E + 10.0 * N) * cw_iters  # 32 E + 10 N per codeword-iteration
+    iter_moved = (moved["check"] + moved["variable"]) * cw_iters
     per_cwi, traffic_src = find_traffic(names[dom])
     traffic = round(per_cwi * cw_iters / k_launch) if per_cwi else None
     # measured ceiling of the dominant kernel's access shape: the resident pool's in-place passes
@@ -280,7 +325,18 @@ def roofline(eng, G, st, cw_iters, coded=False, cpw=None) -> dict:
         "algorithmic_bytes_per_cw_iter": by_kernel[dom],
         "bytes_per_launch": round(bytes_per_launch), "avg_launch_ms": round(k_avg, 4),
         "launch_unit": "kernel launch",
+        "achieved_moved": round(achieved_moved, 1) if achieved_moved else None,
+        "frac_moved": round(achieved_moved / HBM_PEAK_GBS, 4) if achieved_moved else None,
+        "moved_bytes_per_cw_iter": moved[dom],
         "iteration_GBps": round(iter_bytes / (it_ms * 1e-3) / 1e9, 1) if it_ms > 0 else None,
+        "iteration_GBps_moved": round(iter_moved / (it_ms * 1e-3) / 1e9, 1) if it_ms > 0 else None,
+        "iteration_bytes_per_cw_iter": {"survey_8d": 32.0 * E + 10.0 * N,
+                                        "moved": moved["check"] + moved["variable"]},
+        "iteration_note": ("iteration_GBps: SURVEY 8(d)'s 32 E + 10 N bytes per codeword-iteration (fp64 "
+                           "messages both ways, fp64 prior) over the iteration's kernel time (check + variable "
+                           "+ syndrome); iteration_GBps_moved: the bytes the check and variable kernels move"
+                           + (" (compressed min-sum: per-row records instead of E fp64 c2v, so the SURVEY "
+                              "rate may exceed the 8 TB/s peak)" if eng.msa_compressed else "")),
         "kernels": names,
         "avg_ms": {k: round(avg_ms(k), 4) for k in st},
         "launches": {k: v["launches"] for k, v in st.items()},
@@ -463,17 +519,45 @@ def msa_1m(args, og, threads, cw, d_cw):
             h = d_hard.download(np.empty((k, N), np.uint8), offset=start * N)
             return h, iters[start:start + k], valid[start:start + k]
 
-        checked, bad, _ = oracle_check(og, llr_fn, gpu_out, 1, max_iter, [(0, n // 2), (B - n // 2, n // 2)], threads)
+        tail, inter = tail_and_interior(B, n // 2, n_tail=n // 2, seed=args.seed)
+        checked, bad, _ = oracle_check(og, llr_fn, gpu_out, 1, max_iter, [(0, n // 2), tail, inter], threads)
         out["check"] = {"checked": checked, "mismatches": len(bad), "first_mismatches": bad[:8],
-                        "what": "hard bits, iterations, valid flags of the timed decode vs the oracle, both ends"}
+                        "rows": {"head": [0, n // 2], "tail": [int(tail[0]), B] if tail.size else None,
+                                 "interior": inter.tolist()},
+                        "what": "hard bits, iterations, valid flags of the timed decode vs the oracle: both ends "
+                                "of the batch and random interior codewords"}
     for b in (d_in, d_hard, d_iters, d_valid):
         b.free()
     eng.close()
     return out
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` run without a launcher: start N ranks under
+    torch.distributed.run as a CHILD process (this process has not touched
+    the GPU and never execs), forward rank 0's JSON line to stdout and
+    everything else to stderr, and return the child's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench.py: --gpus {n} without a launcher: running {n} ranks under torch.distributed.run",
+          file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    for line in p.stdout:
+        print(line.rstrip("\n"), file=sys.stdout if line.lstrip().startswith("{") else sys.stderr, flush=True)
+    return p.wait()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and args.workload == "bsc" and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     cpus = host_cpus()
     if args.workload == "dna272":
         og = _oracle().OracleGraph(os.path.join(ROOT, "tests", "golden", "decode_n18432_m2048_final.pchk")) \
@@ -518,7 +602,7 @@ def main():
     dev = local % max(1, L.device_count())
     algo = args.algo
     opt = lambda v: None if v < 0 else bool(v)  # noqa: E731
-    eng = L.Engine(G, dev, algo, chunk=args.chunk, group_tiles=args.group_tiles if args.group_tiles >= 0 else None,
+    eng = L.Engine(G, dev, algo, chunk=args.chunk, group_tiles=args.group_tiles,
                    nontemporal=opt(args.nt), continuous=opt(args.cont), resident=opt(args.res),
                    var_cpw=args.var_cpw or None)
     cw = synth.load_codewords()
@@ -595,17 +679,20 @@ def main():
 
     threads = max(1, cpus["effective"] // max(1, local_world))
     if world == 1 and args.cpu_baseline:
-        out["cpu_baseline"], (checked, bad) = cpu_baseline(args, og, llr_fn, B, gpu_out, cpus)
+        out["cpu_baseline"], (checked, bad, rows) = cpu_baseline(args, og, llr_fn, B, gpu_out, cpus)
     else:
         n = min(B, max(2, args.check_per_thread * threads))
-        checked, bad, _ = oracle_check(og, llr_fn, gpu_out, a, args.max_iter, [(0, n - n // 2), (B - n // 2, n // 2)],
-                                       threads)
+        head = n - n // 2
+        tail, inter = tail_and_interior(B, head, n_tail=n // 2, seed=args.seed + rank)
+        checked, bad, _ = oracle_check(og, llr_fn, gpu_out, a, args.max_iter, [(0, head), tail, inter], threads)
+        rows = {"head": [0, head], "tail": [int(tail[0]), B] if tail.size else None, "interior": inter.tolist()}
     per = grp.gather({"rank": rank, "b0": b0, "B": B, "checked": checked, "mismatches": len(bad),
-                      "first_mismatches": [b0 + k for k in bad[:4]], "threads": threads})
+                      "first_mismatches": [b0 + k for k in bad[:4]], "threads": threads, "rows": rows})
     out["check"] = {"checked": sum(p["checked"] for p in per), "mismatches": sum(p["mismatches"] for p in per),
                     "per_rank": per,
                     "what": "hard bits, iteration counts and valid flags of the timed GPU decode vs the oracle, on "
-                            "a sample of every rank's own shard (N = 1: the cpu_baseline sample)"}
+                            "every rank's own shard: its head (N = 1: the cpu_baseline sample), its last rows (the "
+                            "lane pool's drain) and random interior rows (per_rank[].rows, shard-relative)"}
     mismatches = out["check"]["mismatches"]
 
     # ---- secondary legs (N = 1): config 3 on fp64 input, config 5 and config 2, each checked ----

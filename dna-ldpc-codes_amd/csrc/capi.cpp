@@ -130,9 +130,10 @@ double llr_unit(const double* src, int64_t rows, size_t N)
 }
 
 // codes of LLRs [i0, i1) (host_simd.cpp)
-bool encode_rows(const double* __restrict__ src, int8_t* __restrict__ code, size_t i0, size_t i1, double unit)
+bool encode_rows(const double* __restrict__ src, int8_t* __restrict__ code, size_t i0, size_t i1, double unit,
+                 bool msa)
 {
-    return ldpc::host_encode_lattice(src, code, i0, i1, unit, kCodeMax);
+    return ldpc::host_encode_lattice(src, code, i0, i1, unit, kCodeMax, /*keep_neg_zero=*/msa);
 }
 
 // byte x -> 8 bytes, byte r = bit r of x (unpacking the device's packed hard bits)
@@ -216,7 +217,7 @@ int make_slot(const HostGraph* g, int device, int algo, int64_t pool, int64_t xf
     s->algo = algo;
     s->sched = sched;
     s->eng = std::make_unique<Engine>();
-    int rc = s->eng->init(g, device, algo, pool, &sched);
+    int rc = s->eng->init(g, device, algo, pool, &sched, /*resolved=*/true);
     if (rc) return rc;
     s->pool = pool;
     s->xfer = xfer;
@@ -482,7 +483,7 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
         // PCIe in double-buffered chunks of `xfer`.
         const int64_t sh64 = (shard + 63) / 64 * 64;
         const int64_t pool = o.chunk > 0 ? o.chunk : (shard <= kExplicitPoolMax ? sh64 : 0);
-const int64_t xfer = std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool + 63) / 64 * 64));
+        const int64_t xfer = std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool + 63) / 64 * 64));
         std::unique_ptr<Slot> slot = g->take(dev, algo, pool, xfer, o.chunk <= 0 && pool > 0, sched);
         int rc = LDPC_OK;
         if (!slot) rc = make_slot(&g->h, dev, algo, pool, xfer, sched, slot);
@@ -519,7 +520,8 @@ const int64_t xfer = std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool
                     for (int64_t pc = 0; pc < pieces && ok; pc++) {
                         const int64_t p0 = Bc * pc / pieces, p1 = Bc * (pc + 1) / pieces;
                         parallel_rows(W, p1 - p0, [&](int64_t r0, int64_t r1) {
-                            if (!encode_rows(src, S.h_code[k], (size_t)(p0 + r0) * N, (size_t)(p0 + r1) * N, unit))
+                            if (!encode_rows(src, S.h_code[k], (size_t)(p0 + r0) * N, (size_t)(p0 + r1) * N, unit,
+                                             algo == LDPC_ALGO_MSA))
                                 ok = false;
                         });
                         if (ok)
@@ -597,7 +599,8 @@ const int64_t xfer = std::min<int64_t>(sh64, std::max<int64_t>(kXferChunk, (pool
             LDPC_HIP(hipStreamWaitEvent(E.stream, S.ev_h2d[k], 0));
             const double td0 = api_timing ? now() : 0;
             int r = S.coded[k] ? E.decode_codes(S.d_code[k], S.h_table[k].data(), LDPC_IN_LLR, Bc, max_iter, S.d_hard[k],
-                                                post_out ? S.d_post[k] : nullptr, o.post_kind, S.d_iters[k], S.d_valid[k])
+                                                post_out ? S.d_post[k] : nullptr, o.post_kind, S.d_iters[k], S.d_valid[k],
+                                                S.d_in[k])
                                : E.decode(S.d_in[k], in_kind, Bc, max_iter, S.d_hard[k],
                                           post_out ? S.d_post[k] : nullptr, o.post_kind, S.d_iters[k], S.d_valid[k]);
             if (r) return r;

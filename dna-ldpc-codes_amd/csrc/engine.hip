@@ -55,16 +55,17 @@ constexpr int32_t kDefaultFlags = LDPC_SCHED_NONTEMPORAL | LDPC_SCHED_CONTINUOUS
                                   LDPC_SCHED_RESIDENT | LDPC_SCHED_FIRST_FROM_PRIOR | LDPC_SCHED_LR_TABLE;
 constexpr int32_t kAllFlags = kDefaultFlags | LDPC_SCHED_DEBUG_NO_DRAIN;
 
-// flags_set bits of a resolved schedule (never set by callers): resolved,
-// and whether the caller chose the resident pool (the auto-disable rule for
-// large explicit pools applies only when it did not)
+// flags_set bits of a resolved schedule, outside kAllFlags: resolved, and
+// whether the caller chose the resident pool (the auto-disable rule for
+// large explicit pools applies only when it did not).  A caller's bits
+// outside kAllFlags are dropped, so no caller can mark a schedule resolved.
 constexpr int32_t kResolved = 1 << 30, kResChosen = 1 << 29;
 
 ldpc_schedule resolve_schedule(const ldpc_schedule* s)
 {
-    if (s && (s->flags_set & kResolved)) return *s;  // idempotent
     ldpc_schedule r{};
     if (s) r = *s;
+    r.flags_set &= kAllFlags;
     r.flags = (kDefaultFlags & ~r.flags_set) | (r.flags & r.flags_set);
     r.flags &= kAllFlags;
     r.flags_set = kAllFlags | kResolved | ((r.flags_set & LDPC_SCHED_RESIDENT) ? kResChosen : 0);
@@ -152,12 +153,20 @@ static uint16_t* msa_meta(double* scratch, int64_t tiles, int32_t M)
     return reinterpret_cast<uint16_t*>(scratch + (size_t)tiles * M * dev::MSA_REC_PLANES * dev::TILE);
 }
 
-int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, const ldpc_schedule* schedule)
+int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, const ldpc_schedule* schedule,
+                 bool resolved)
 {
     g = graph;
     device = dev;
     algo = algorithm;
-    sched = resolve_schedule(schedule);
+    if (resolved && schedule && (schedule->flags_set & kResolved)) {
+        sched = *schedule;  // the host API's slot: resolved once per call (capi.cpp)
+        sched.pool_tiles = std::max(sched.pool_tiles, 1);
+        sched.poll_every = std::max(sched.poll_every, 1);
+        sched.syn_blocks = std::min(std::max(sched.syn_blocks, 1), 256);
+    } else {
+        sched = resolve_schedule(schedule);
+    }
     if (algo < LDPC_ALGO_BP || algo > LDPC_ALGO_GALLAGER_B2) { set_error("unknown algorithm"); return LDPC_ERR_ARG; }
     const bool int_algo = algo >= LDPC_ALGO_QMSA;
     int ndev = 0;
@@ -698,7 +707,8 @@ int Engine::run_chunk_int(const double* d_in, int64_t Bc, int64_t b_base, int32_
 // one pass of <= cap codewords at a time.  Either way each codeword sees
 // exactly the prior values the table gives its codes.
 int Engine::decode_codes(const int8_t* d_codes, const double* h_table, int table_kind, int64_t B, int32_t max_iter,
-                         uint8_t* d_hard, double* d_post, int post_kind, int32_t* d_iters, uint8_t* d_valid)
+                         uint8_t* d_hard, double* d_post, int post_kind, int32_t* d_iters, uint8_t* d_valid,
+                         double* d_stage)
 {
     if (B < 0 || max_iter < 0) { set_error("B and max_iter must be >= 0"); return LDPC_ERR_ARG; }
     if (!h_table || (B > 0 && !d_codes)) { set_error("decode_codes: null codes or table"); return LDPC_ERR_ARG; }
@@ -731,14 +741,28 @@ int Engine::decode_codes(const int8_t* d_codes, const double* h_table, int table
         cur_codes = nullptr;
         return rc;
     }
+    // fp64 staging of one pass: the caller's (the host API's d_in) or the
+    // engine's own, sized to the largest pass seen
     const size_t N = (size_t)g->N;
-    if (!d_expand) LDPC_HIP(hipMalloc((void**)&d_expand, (size_t)cap * N * sizeof(double)));
+    const int64_t pass = std::min<int64_t>(cap, B);
+    double* stage = d_stage;
+    if (!stage) {
+        if (expand_rows < pass) {
+            LDPC_HIP(hipStreamSynchronize(stream));  // a previous decode may still read it
+            LDPC_HIP(hipFree(d_expand));
+            d_expand = nullptr;
+            expand_rows = 0;
+            LDPC_HIP(hipMalloc((void**)&d_expand, (size_t)pass * N * sizeof(double)));
+            expand_rows = pass;
+        }
+        stage = d_expand;
+    }
     const int64_t tb = tie_base;
     for (int64_t b0 = 0; b0 < B; b0 += cap) {
         const int64_t Bc = std::min<int64_t>(cap, B - b0);
-        if (int rc = expand_lr(d_codes + (size_t)b0 * N, d_ptab, d_expand, Bc * (int64_t)N, stream)) return rc;
+        if (int rc = expand_lr(d_codes + (size_t)b0 * N, d_ptab, stage, Bc * (int64_t)N, stream)) return rc;
         tie_base = tb + b0;  // the integer decoders' tie hash keys on the index in the whole call
-        const int rc = decode(d_expand, in_kind, Bc, max_iter, d_hard ? d_hard + (size_t)b0 * N : nullptr,
+        const int rc = decode(stage, in_kind, Bc, max_iter, d_hard ? d_hard + (size_t)b0 * N : nullptr,
                               d_post ? d_post + (size_t)b0 * N : nullptr, post_kind, d_iters ? d_iters + b0 : nullptr,
                               d_valid ? d_valid + b0 : nullptr);
         tie_base = tb;

@@ -31,7 +31,8 @@ enum KClass { K_CHECK = 0, K_VAR = 1, K_SYN = 2, K_INIT = 3, K_FINAL = 4, K_OTHE
 
 // A caller's ldpc_schedule with every field resolved: flags_set covers all
 // bits, zero fields replaced by the defaults (include/ldpc_amd.h).  Two
-// resolved schedules compare equal iff they select the same engine.
+// resolved schedules compare equal iff they select the same engine.  The
+// input is always treated as a caller's (bits outside LDPC_SCHED_* dropped).
 ldpc_schedule resolve_schedule(const ldpc_schedule* s);
 inline bool sched_flag(const ldpc_schedule& s, int bit) { return (s.flags & bit) != 0; }
 
@@ -100,7 +101,8 @@ struct Engine {
     double* d_ptab = nullptr;
     double* h_ptab = nullptr;
     bool ptab_valid = false;
-    double* d_expand = nullptr;
+    double* d_expand = nullptr;  // fp64 staging of decode_codes' fixed passes (expand_rows codewords)
+    int64_t expand_rows = 0;
     const int8_t* cur_codes = nullptr;
     // integer decoders (LDPC_ALGO_QMSA / GALLAGER_*): int32 views of v2c, c2v, prior
     int32_t q_precision = 6, q_beta = 0;
@@ -117,7 +119,10 @@ struct Engine {
     double ms[K_NCLASS] = {0};
 
     ~Engine();
-    int init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, const ldpc_schedule* schedule);
+    // schedule: a caller's (resolved here), or with `resolved` one that
+    // resolve_schedule already returned (the host API's slots)
+    int init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, const ldpc_schedule* schedule,
+             bool resolved = false);
     int run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
                  int post_kind, int32_t* d_iters, uint8_t* d_valid);
     // decode Bc <= cap codewords whose [Bc][N] input is at d_in (device)
@@ -127,9 +132,12 @@ struct Engine {
                int post_kind, int32_t* d_iters, uint8_t* d_valid);
     // coded input: d_codes [B][N] int8 on device, h_table[256] (host) the
     // channel value of code k at k + 128, of kind table_kind (LDPC_IN_LLR or,
-    // BP only, LDPC_IN_LR); BP takes the host exp of an LLR table
+    // BP only, LDPC_IN_LR); BP takes the host exp of an LLR table.  d_stage
+    // (optional, >= min(cap, B) x N fp64): where schedules without coded
+    // kernels expand a pass to fp64 (else an engine buffer)
     int decode_codes(const int8_t* d_codes, const double* h_table, int table_kind, int64_t B, int32_t max_iter,
-                     uint8_t* d_hard, double* d_post, int post_kind, int32_t* d_iters, uint8_t* d_valid);
+                     uint8_t* d_hard, double* d_post, int post_kind, int32_t* d_iters, uint8_t* d_valid,
+                     double* d_stage = nullptr);
     // integer decoders, Bc <= cap codewords; b_base = global index of the first (tie hash)
     int run_chunk_int(const double* d_in, int64_t Bc, int64_t b_base, int32_t max_iter, uint8_t* d_hard,
                       double* d_post, int32_t* d_iters, uint8_t* d_valid);

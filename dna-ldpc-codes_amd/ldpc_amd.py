@@ -515,14 +515,14 @@ class Engine:
     """Device-resident decoder (ldpc_engine_*): one device, one HIP stream.
     The schedule comes from `schedule` (a Schedule or dict) and/or the
     keyword shortcuts (group_tiles, nontemporal, continuous, resident, ...,
-    any Schedule.make keyword); unset ones keep the library defaults."""
+    any Schedule.make keyword); unset ones keep the library defaults.  Values
+    pass through as the ABI defines them (group_tiles 0 = default, < 0 = the
+    whole pass)."""
 
     def __init__(self, g: Graph, device: int = 0, algo="bp", chunk: int = 0, schedule=None, **sched_kw):
         self.g, self.device, self.algo = g, device, _algo(algo)
         kw = dict(_schedule_kw(schedule))
         kw.update({k: v for k, v in sched_kw.items() if v is not None})
-        if kw.get("group_tiles") is not None and kw["group_tiles"] < 0:
-            kw.pop("group_tiles")  # -1: default (the ABI's 0)
         sch = Schedule.make(**kw)
         err = C.c_int(0)
         self._h = lib().ldpc_engine_create_ex(g.handle, device, self.algo, chunk, C.byref(sch), C.byref(err))

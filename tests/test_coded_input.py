@@ -184,10 +184,11 @@ def test_coded_nonfinite_table_entries(gpu, G, codewords, algo):
 
 @pytest.mark.parametrize("algo", ["bp", "msa"])
 def test_host_api_negative_zero_and_off_lattice(G, og, codewords, algo):
-    """ldpc_decode's code table path takes only exact lattice batches: a -0.0
-    LLR (equal to 0 * unit, other bits; min-sum sums keep a zero's sign) or an
-    off-lattice value sends the batch through the fp64 path; results equal the
-    oracle bit for bit, posterior included."""
+    """ldpc_decode's code table path takes only exact lattice batches: for
+    min-sum a -0.0 LLR (equal to 0 * unit, other bits; min-sum sums keep a
+    zero's sign) and for both an off-lattice value send the batch through the
+    fp64 path (BP keeps -0.0 on the code path: exp(-0.0) == exp(0.0)); results
+    equal the oracle bit for bit, posterior included."""
     a = 0 if algo == "bp" else 1
     llr = synth.dna_like_llrs(codewords, seed=12, reads=57000)[:96].copy()
     zeros = np.argwhere(llr == 0)

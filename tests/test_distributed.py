@@ -67,3 +67,22 @@ def test_two_rank_gloo_matches_single_process(og, codewords):
     llr = synth.bsc_llrs(codewords, 0, total, seed=2026, p=0.006)
     h, _, it, v = og.decode_batch(llr, 20, threads=4, want_post=False)
     assert np.array_equal(hard, h) and np.array_equal(iters, it)
+
+
+@pytest.mark.timeout(180)
+def test_plain_bench_gpus_n_starts_n_ranks():
+    """`python bench.py --gpus 2` without a launcher starts two ranks under
+    torch.distributed.run as a child process and forwards its exit code.  On
+    this GPU-less host both ranks join the gloo group and then fail at engine
+    creation (no device), which must surface as a non-zero exit, not as a
+    one-process measurement."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--global-batch", "128",
+                        "--steps", "1", "--warmup", "0", "--cpu-baseline", "0"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=170)
+    assert "running 2 ranks under torch.distributed.run" in r.stderr
+    assert r.returncode != 0 and not r.stdout.strip(), (r.returncode, r.stdout)
+    assert r.stderr.count("ldpc_amd error") >= 2, r.stderr[-3000:]

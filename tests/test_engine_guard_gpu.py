@@ -25,3 +25,23 @@ def test_undrained_decode_is_bounded(gpu, og, codewords, algo, sch):
         G2.decode(llr, max_iter=5, algo=algo, post=None, schedule=dict(sch, debug_no_drain=True))
     assert e.value.code == L.LDPC_ERR_DEVICE and "did not drain" in str(e.value)
     _cmp(G2, og, llr, 5, algo=algo, schedule=sch)
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("algo", ["bp", "msa"])
+def test_all_bits_flags_set_is_resolved(gpu, G, og, codewords, algo):
+    """A caller's schedule with every flags_set bit on (-1: 'take every flag
+    from flags') is still resolved: bits outside LDPC_SCHED_* are dropped, so
+    it cannot pose as an already-resolved schedule and skip the defaults of
+    poll_every / syn_blocks / pool_tiles (which would divide by zero or launch
+    an empty grid).  Through ldpc_decode and ldpc_engine_create_ex; a batch
+    larger than 8 pools exercises the resident pool's polling cadence."""
+    L = gpu
+    s = L.Schedule()
+    s.flags_set = -1
+    s.flags = L.SCHED_FLAGS["continuous"] | L.SCHED_FLAGS["resident"] | L.SCHED_FLAGS["msa_compressed"]
+    llr = synth.bsc_llrs(codewords, 0, 8 * 192 + 70, seed=4, p=0.004)
+    _cmp(G, og, llr, 6, algo=algo, schedule=s)
+    eng = L.Engine(G, 0, algo, schedule=s)
+    assert eng.continuous and eng.flags & ~0x7FFF == 0
+    eng.close()

@@ -91,3 +91,50 @@ def test_config3_exact_workload(gpu, G, og, codewords):
         h = np.empty((1, N), np.uint8)
         dh.download(h, offset=int(b) * N)
         assert np.array_equal(h[0], rh[k]), int(b)
+
+
+@pytest.mark.timeout(300)
+def test_config5_exact_workload(gpu, G, og, codewords):
+    """SURVEY 8(d) config 5 exactly as bench.py's secondary leg times it: 1M
+    codewords of BSC p = 0.002 (seed 2026) as int8 channel codes, float
+    min-sum with early termination (Run_MSA_Decoder_INF, dec.cpp:1216-1250),
+    50 iterations, the engine's default schedule (compressed messages,
+    1024-lane refill pool).  Properties over the whole batch (iteration
+    counts, valid flags), GF(2) syndromes of hard rows from both ends and the
+    interior, and 64 codewords (both ends of the batch + random interior
+    ones) equal to the oracle bit for bit."""
+    L = gpu
+    B, N, max_iter, seed, p = 1_000_000, G.N, 50, 2026, 0.002
+    eng = L.Engine(G, 0, "msa")
+    assert eng.msa_compressed and eng.continuous
+    cwbuf = L.DeviceBuffer(0, codewords.nbytes)
+    cwbuf.upload(codewords)
+    table = np.arange(-128, 128, dtype=np.float64) * synth.LLR_UNIT
+    din = L.DeviceBuffer(0, B * N)
+    dh, dit, dv = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
+    eng.gen_bsc_codes(din.at(0), 0, B, cwbuf.at(0), 272, seed, p)
+    eng.decode_codes(din.at(0), table, L.IN_LLR, B, max_iter, dh.at(0), None, L.POST_LLR, dit.at(0), dv.at(0))
+    eng.sync()
+    it = dit.download(np.empty(B, np.int32))
+    v = dv.download(np.empty(B, np.uint8)).astype(bool)
+    assert (it >= 0).all() and (it <= max_iter).all()
+    assert (it[~v] == max_iter).all(), "an invalid codeword stopped early"
+    assert 0.99 < v.mean() < 1.0, v.mean()
+    assert 10 < it.mean() < 16, it.mean()
+    H = _H(G)
+    for b0 in (0, B // 2 - 2048, B - 4096):
+        h = dh.download(np.empty((4096, N), np.uint8), offset=b0 * N)
+        syn = (H @ h.T.astype(np.int32)) % 2
+        vv = v[b0:b0 + 4096]
+        assert not syn[:, vv].any(), "a codeword reported valid has a nonzero syndrome"
+        assert syn[:, ~vv].any(axis=0).all(), "an invalid codeword has a zero syndrome"
+    rng = np.random.default_rng(seed)
+    idx = np.unique(np.concatenate([np.arange(16), np.arange(B - 16, B), rng.choice(B, 32, replace=False)]))
+    llr = np.concatenate([synth.bsc_llrs(codewords, int(b), 1, seed=seed, p=p) for b in idx])
+    rh, _, rit, rv = og.decode_batch(llr, max_iter, algo=1, threads=8, want_post=False)
+    for k, b in enumerate(idx):
+        h = dh.download(np.empty((1, N), np.uint8), offset=int(b) * N)
+        assert np.array_equal(h[0], rh[k]) and it[b] == rit[k] and v[b] == bool(rv[k]), int(b)
+    for b in (din, dh, dit, dv, cwbuf):
+        b.free()
+    eng.close()

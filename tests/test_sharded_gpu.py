@@ -43,39 +43,74 @@ def _load(d, world, N):
     return parts
 
 
-@pytest.mark.timeout(240)
-def test_two_rank_bench_shards_match_single_process(gpu, G, tmp_path):
-    total, args = 1000, ["--global-batch", "1000", "--max-iter", "20", "--p", "0.0065", "--steps", "1",
-                         "--warmup", "0", "--no-profile", "--cpu-baseline", "0"]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
-    d2, d1 = str(tmp_path / "two"), str(tmp_path / "one")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dump-dir", d2, *args],
-                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+SHARD_ARGS = ["--global-batch", "1000", "--max-iter", "20", "--p", "0.0065", "--steps", "1", "--warmup", "0",
+              "--no-profile", "--cpu-baseline", "0"]
+LAUNCH_ENV = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_PORT",
+              "TORCHELASTIC_RUN_ID")
+
+
+def _env():
+    env = {k: v for k, v in os.environ.items() if k not in LAUNCH_ENV}
+    env.update(HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    return env
+
+
+@pytest.fixture(scope="module")
+def single_process_dump(tmp_path_factory):
+    """One single-process bench.py decode of the whole global range [0, 1000)."""
+    d1 = str(tmp_path_factory.mktemp("one"))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dump-dir", d1, *SHARD_ARGS], cwd=ROOT,
+                       env=_env(), capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-3000:]
-    out2 = _line(r.stdout)
+    out1 = _line(r.stdout)
+    assert out1["n_gpus"] == 1 and out1["config"]["per_rank"] == [1000]
+    one = _load(d1, 1, None)[0]
+    assert len(np.unique(one["iters"])) > 2 and one["valid"].any()
+    return one
+
+
+def _check_two_rank_run(stdout, d2, one):
+    out2 = _line(stdout)
     assert out2["n_gpus"] == 2 and out2["scaling"] == "strong"
-    assert out2["config"]["per_rank"] == [500, 500] and out2["config"]["global_batch"] == total
-    # every rank checked a sample of its own shard against the oracle
+    assert out2["config"]["per_rank"] == [500, 500] and out2["config"]["global_batch"] == 1000
+    # every rank checked its own shard against the oracle: head, tail, interior
     ck = out2["check"]
     assert ck["mismatches"] == 0 and [p["rank"] for p in ck["per_rank"]] == [0, 1]
     assert [p["b0"] for p in ck["per_rank"]] == [0, 500] and all(p["checked"] >= 16 for p in ck["per_rank"])
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dump-dir", d1, *args], cwd=ROOT, env=env,
-                       capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stderr[-3000:]
-    out1 = _line(r.stdout)
-    assert out1["n_gpus"] == 1 and out1["config"]["per_rank"] == [total]
-    two = _load(d2, 2, G.N)
-    one = _load(d1, 1, G.N)[0]
+    for p in ck["per_rank"]:
+        assert p["rows"]["tail"][1] == 500 and len(p["rows"]["interior"]) > 0
+    two = _load(d2, 2, None)
     assert [int(z["b0"]) for z in two] == [0, 500] and [int(z["B"]) for z in two] == [500, 500]
     for z in two:
         b0, B = int(z["b0"]), int(z["B"])
         assert np.array_equal(z["iters"], one["iters"][b0:b0 + B])
         assert np.array_equal(z["valid"], one["valid"][b0:b0 + B])
         assert np.array_equal(z["hard"], one["hard"][b0:b0 + B])
-    it = one["iters"]
-    assert len(np.unique(it)) > 2 and one["valid"].any()
+
+
+@pytest.mark.timeout(240)
+def test_two_rank_bench_shards_match_single_process(gpu, single_process_dump, tmp_path):
+    """bench.py under an explicit torch.distributed.run (the driver's N > 1 form)."""
+    d2 = str(tmp_path / "two")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dump-dir", d2, *SHARD_ARGS],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check_two_rank_run(r.stdout, d2, single_process_dump)
+
+
+@pytest.mark.timeout(240)
+def test_plain_bench_gpus2_runs_two_ranks(gpu, single_process_dump, tmp_path):
+    """A plain `python bench.py --gpus 2` (no launcher in the environment)
+    starts the two ranks itself (DNA_main.cpp:629-651's per-rank split, one
+    process per GPU) and reports n_gpus 2 with both ranks' oracle checks."""
+    d2 = str(tmp_path / "two")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dump-dir", d2,
+                        *SHARD_ARGS], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "running 2 ranks under torch.distributed.run" in r.stderr
+    _check_two_rank_run(r.stdout, d2, single_process_dump)
 
 
 def test_bench_global_batch_odd_split(gpu, tmp_path):
