@@ -90,6 +90,8 @@ def parse():
     ap.add_argument("--res", type=int, default=-1,
                     help="resident in-place pool of a few tiles (-1: engine default; BP / fp64 min-sum, continuous)")
     ap.add_argument("--var-cpw", type=int, default=0, help="columns per variable-phase wave (0: engine default 4)")
+    ap.add_argument("--ffp", type=int, default=-1,
+                    help="first check from the prior / codes (LDPC_SCHED_FIRST_FROM_PRIOR; -1: engine default)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
     ap.add_argument("--secondary", type=int, default=1,
                     help="N = 1: also time config 2 (DNA batch, host API) and config 5 (1M min-sum) after the headline")
@@ -389,22 +391,37 @@ def dna272(args, og, threads, max_iter=200):
     el = (time.perf_counter() - t) / reps
     it = d_i.download(np.empty(B, np.int32))
     hard = d_h.download(np.empty((B, N), np.uint8))
-    # host API end to end (same decode, LLRs in host memory)
+    # host API end to end (same decode, inputs in host memory): the DNA stage's
+    # count differences k with the table k * ln49 (ldpc_decode_codes), and the
+    # fp64 LLR matrix k * ln49 (ldpc_decode: lattice check + encode on the host)
+    k8 = np.ascontiguousarray(k.astype(np.int8))
+    table = np.arange(-128, 128, dtype=np.float64) * synth.LLR_UNIT
+    assert np.array_equal(table[k8.astype(np.int64) + 128], llr)
+    G.decode_codes(k8, table, max_iter=max_iter, post=None)
     G.decode(llr, max_iter=max_iter, post=None)
-    th = []
+    th, tl = [], []
     for _ in range(15):  # the host leg varies with the box's other tenants: median and min of 15 calls
         t = time.perf_counter()
-        h2, _, it2, v2 = G.decode(llr, max_iter=max_iter, post=None)
+        h2, _, it2, v2 = G.decode_codes(k8, table, max_iter=max_iter, post=None)
         th.append(time.perf_counter() - t)
+        t = time.perf_counter()
+        h3, _, it3, v3 = G.decode(llr, max_iter=max_iter, post=None)
+        tl.append(time.perf_counter() - t)
     assert np.array_equal(h2, hard) and np.array_equal(it2, it)
+    assert np.array_equal(h3, hard) and np.array_equal(it3, it) and np.array_equal(v3, v2)
     out = {"workload": f"dna272-bp{max_iter}", "batch": B, "max_iter": max_iter, "input": args.input,
            "value": round(B / el, 1), "unit": "codewords/s", "ms_per_decode_device": round(el * 1e3, 3),
            "mean_iters": round(float(it.mean()), 3), "genie_ok": int((hard == cw).all(axis=1).sum()),
            "host_api_ms_median": round(float(np.median(th)) * 1e3, 3),
            "host_api_ms_min": round(float(np.min(th)) * 1e3, 3),
            "host_api_calls": len(th),
-           "host_api_includes": "ldpc_decode end to end: host encode of the k*ln49 alphabet to int8 codes (else host "
-                                "exp) + H2D + decode + packed hard-bit D2H + unpack"}
+           "host_api_includes": "Graph.decode_codes -> ldpc_decode_codes end to end: the int8 count differences k "
+                                "and the table k*ln49 (decoder.py:314) copied to pinned staging + H2D + decode + "
+                                "packed hard-bit D2H + unpack",
+           "host_api_llr_ms_median": round(float(np.median(tl)) * 1e3, 3),
+           "host_api_llr_ms_min": round(float(np.min(tl)) * 1e3, 3),
+           "host_api_llr_includes": "Graph.decode -> ldpc_decode from the fp64 LLR matrix: host lattice check + "
+                                    "encode to int8 codes, then as above"}
     if og is not None:
         t = time.perf_counter()
         rh, _, rit, rv = og.decode_batch(llr, max_iter, threads=threads, want_post=False)
@@ -484,7 +501,7 @@ def msa_1m(args, og, threads, cw, d_cw):
     G = L.Graph(synth.PCHK)
     N = G.N
     B, p, max_iter = args.msa_batch, 0.002, 50
-    eng = L.Engine(G, 0, "msa")
+    eng = L.Engine(G, 0, "msa", first_from_prior=None if args.ffp < 0 else bool(args.ffp))
     d_in, decode = channel(L, eng, args, 0, N, 0, B, d_cw, cw.shape[0], p, L.IN_LLR)
     d_hard, d_iters, d_valid = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
 
@@ -508,6 +525,7 @@ def msa_1m(args, og, threads, cw, d_cw):
            "value": round(B * steps / el, 1), "unit": "codewords/s", "ms_per_step": round(el / steps * 1e3, 2),
            "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 5),
            "resident_per_pass": eng.cap, "group_tiles": eng.group_tiles, "compressed_msa": eng.msa_compressed,
+           "first_check_from_codes": bool(eng.msa_compressed and eng.first_from_prior and args.input == "code"),
            "roofline": roofline(eng, G, st, cw_iters, args.input == "code")}
     if og is not None:
         n = max(8, 4 * threads)
@@ -604,7 +622,7 @@ def main():
     opt = lambda v: None if v < 0 else bool(v)  # noqa: E731
     eng = L.Engine(G, dev, algo, chunk=args.chunk, group_tiles=args.group_tiles,
                    nontemporal=opt(args.nt), continuous=opt(args.cont), resident=opt(args.res),
-                   var_cpw=args.var_cpw or None)
+                   var_cpw=args.var_cpw or None, first_from_prior=opt(args.ffp))
     cw = synth.load_codewords()
     d_cw = L.DeviceBuffer(dev, cw.nbytes)
     d_cw.upload(cw)

@@ -177,7 +177,8 @@ struct Slot {
     uint8_t* d_hbits[2] = {};
     int8_t* h_code[2] = {};   // code table path: one byte per LLR
     int8_t* d_code[2] = {};
-    std::vector<double> h_table[2];  // [kTable] LLR of code k at k + 128
+    std::vector<double> h_table[2];  // [kTable] LLR (or, BP, LR: table_kind) of code k at k + 128
+    int table_kind[2] = {LDPC_IN_LLR, LDPC_IN_LLR};
     bool coded[2] = {};              // the staging buffer holds codes (else fp64 input)
     std::unique_ptr<Workers> workers;
 
@@ -197,6 +198,16 @@ struct Slot {
         if (copy) hipStreamDestroy(copy);
         if (copy_out) hipStreamDestroy(copy_out);
         eng.reset();
+    }
+    // code staging of the integer decoders (ldpc_decode_codes): on first use
+    int want_codes(size_t N)
+    {
+        for (int k = 0; k < 2 && !h_code[k]; k++) {
+            LDPC_HIP(hipHostMalloc((void**)&h_code[k], (size_t)xfer * N, hipHostMallocDefault));
+            LDPC_HIP(hipMalloc((void**)&d_code[k], (size_t)xfer * N));
+            h_table[k].assign(kTable, 0.0);
+        }
+        return LDPC_OK;
     }
     // posterior staging is allocated on the first call that asks for it
     int want_post(size_t N)
@@ -431,13 +442,29 @@ int ldpc_graph_syndrome(const ldpc_graph* g, const uint8_t* dblk, uint8_t* pchk)
     return ldpc::syndrome_host(g->h, dblk, pchk);
 }
 
-int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_iter, int32_t algo,
-                uint8_t* hard_out, double* post_out, int32_t* iters_out, uint8_t* valid_out, const ldpc_opts* opts)
+// The channel input of a host-buffer decode: fp64 LLRs (ldpc_decode) or int8
+// codes with their 256-entry table (ldpc_decode_codes).
+struct HostInput {
+    const double* llr = nullptr;
+    const int8_t* codes = nullptr;
+    const double* table = nullptr;
+    int table_kind = LDPC_IN_LLR;
+};
+
+static int host_decode(const ldpc_graph* gc, const HostInput& in, int64_t B, int32_t max_iter, int32_t algo,
+                       uint8_t* hard_out, double* post_out, int32_t* iters_out, uint8_t* valid_out,
+                       const ldpc_opts* opts)
 {
     ldpc_graph* g = const_cast<ldpc_graph*>(gc);
+    const double* llr = in.llr;
     if (!g) { set_error("null graph"); return LDPC_ERR_ARG; }
     if (B < 0 || max_iter < 0) { set_error("B and max_iter must be >= 0"); return LDPC_ERR_ARG; }
-    if (B > 0 && (!llr || !hard_out)) { set_error("llr and hard_out are required"); return LDPC_ERR_ARG; }
+    if (B > 0 && ((!llr && !in.codes) || !hard_out)) { set_error("the channel input and hard_out are required"); return LDPC_ERR_ARG; }
+    if (in.codes && !in.table) { set_error("ldpc_decode_codes: null table"); return LDPC_ERR_ARG; }
+    if (in.codes && in.table_kind != LDPC_IN_LLR && !(in.table_kind == LDPC_IN_LR && algo == LDPC_ALGO_BP)) {
+        set_error("table kind: LDPC_IN_LLR, or LDPC_IN_LR for BP");
+        return LDPC_ERR_ARG;
+    }
     if (algo < LDPC_ALGO_BP || algo > LDPC_ALGO_GALLAGER_B2) { set_error("unknown algorithm"); return LDPC_ERR_ARG; }
     ldpc_opts o{};
     o.exp_on_host = 1;
@@ -488,6 +515,7 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
         int rc = LDPC_OK;
         if (!slot) rc = make_slot(&g->h, dev, algo, pool, xfer, sched, slot);
         if (!rc && post_out) rc = slot->want_post(N);
+        if (!rc && in.codes) rc = slot->want_codes(N);
         if (rc) { rcs[di] = rc; msgs[di] = ldpc::last_error(); return; }
         if (!slot->workers || slot->workers->size() != host_threads) slot->workers = std::make_unique<Workers>(host_threads);
         Slot& S = *slot;
@@ -504,10 +532,37 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
         auto prep = [&](int64_t c) -> int {
             const int k = (int)(c & 1);
             const int64_t Bc = cn(c);
-            const double* src = llr + (size_t)c0(c) * N;
             LDPC_HIP(hipSetDevice(dev));
             if (c >= 2) LDPC_HIP(hipEventSynchronize(S.ev_h2d[k]));  // staging buffer free again
             const double tp0 = api_timing ? now() : 0;
+            if (in.codes) {
+                // the caller's codes: into pinned staging and across PCIe in
+                // pieces (each crossing while the next is copied)
+                const int8_t* src = in.codes + (size_t)c0(c) * N;
+                if (c >= 2) LDPC_HIP(hipStreamWaitEvent(S.copy, S.ev_dec[k], 0));
+                const int64_t pieces = std::min<int64_t>(4, Bc);
+                for (int64_t pc = 0; pc < pieces; pc++) {
+                    const int64_t p0 = Bc * pc / pieces, p1 = Bc * (pc + 1) / pieces;
+                    parallel_rows(W, p1 - p0, [&](int64_t r0, int64_t r1) {
+                        std::memcpy(S.h_code[k] + (size_t)(p0 + r0) * N, src + (size_t)(p0 + r0) * N,
+                                    (size_t)(r1 - r0) * N);
+                    });
+                    LDPC_HIP(hipMemcpyAsync(S.d_code[k] + (size_t)p0 * N, S.h_code[k] + (size_t)p0 * N,
+                                            (size_t)(p1 - p0) * N, hipMemcpyHostToDevice, S.copy));
+                }
+                std::copy(in.table, in.table + kTable, S.h_table[k].begin());
+                S.table_kind[k] = in.table_kind;
+                S.coded[k] = true;
+                const double tp1 = api_timing ? now() : 0;
+                LDPC_HIP(hipEventRecord(S.ev_h2d[k], S.copy));
+                if (api_timing) {
+                    LDPC_HIP(hipEventSynchronize(S.ev_h2d[k]));
+                    std::fprintf(stderr, "api chunk %lld: codes copy %.3f ms, + H2D %.3f ms\n", (long long)c,
+                                 tp1 - tp0, now() - tp1);
+                }
+                return LDPC_OK;
+            }
+            const double* src = llr + (size_t)c0(c) * N;
             // code table path: all of the chunk's LLRs exact multiples of one unit
             bool coded = false;
             if ((host_exp || algo == LDPC_ALGO_MSA) && lr_table && S.h_code[k]) {
@@ -530,6 +585,7 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
                     }
                     if (ok) {
                         for (int q = -kCodeMax; q <= kCodeMax; q++) S.h_table[k][q + 128] = (double)q * unit;
+                        S.table_kind[k] = LDPC_IN_LLR;
                         coded = true;
                     }
                 }
@@ -598,7 +654,7 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
             E.tie_base = c0(c);  // tie hash keyed by the codeword's index in this call
             LDPC_HIP(hipStreamWaitEvent(E.stream, S.ev_h2d[k], 0));
             const double td0 = api_timing ? now() : 0;
-            int r = S.coded[k] ? E.decode_codes(S.d_code[k], S.h_table[k].data(), LDPC_IN_LLR, Bc, max_iter, S.d_hard[k],
+            int r = S.coded[k] ? E.decode_codes(S.d_code[k], S.h_table[k].data(), S.table_kind[k], Bc, max_iter, S.d_hard[k],
                                                 post_out ? S.d_post[k] : nullptr, o.post_kind, S.d_iters[k], S.d_valid[k],
                                                 S.d_in[k])
                                : E.decode(S.d_in[k], in_kind, Bc, max_iter, S.d_hard[k],
@@ -663,6 +719,26 @@ int ldpc_decode(const ldpc_graph* gc, const double* llr, int64_t B, int32_t max_
     for (size_t i = 0; i < devs.size(); i++)
         if (rcs[i]) { set_error("device " + std::to_string(devs[i]) + ": " + msgs[i]); return rcs[i]; }
     return LDPC_OK;
+}
+
+int ldpc_decode(const ldpc_graph* g, const double* llr, int64_t B, int32_t max_iter, int32_t algo, uint8_t* hard_out,
+                double* post_out, int32_t* iters_out, uint8_t* valid_out, const ldpc_opts* opts)
+{
+    HostInput in;
+    in.llr = llr;
+    return host_decode(g, in, B, max_iter, algo, hard_out, post_out, iters_out, valid_out, opts);
+}
+
+int ldpc_decode_codes(const ldpc_graph* g, const int8_t* codes, const double* table, int32_t table_kind, int64_t B,
+                      int32_t max_iter, int32_t algo, uint8_t* hard_out, double* post_out, int32_t* iters_out,
+                      uint8_t* valid_out, const ldpc_opts* opts)
+{
+    HostInput in;
+    in.codes = codes;
+    in.table = table;
+    in.table_kind = table_kind;
+    if (B > 0 && !codes) { set_error("null codes"); return LDPC_ERR_ARG; }
+    return host_decode(g, in, B, max_iter, algo, hard_out, post_out, iters_out, valid_out, opts);
 }
 
 int ldpc_engine_set_params(ldpc_engine* e, int32_t msa_precision, double msa_step, int32_t msa_offset,

@@ -98,12 +98,8 @@ __device__ __forceinline__ bool line_occupied(uint64_t m, int lane)
 // (pre-update ballots), one CPW-byte store per lane when the output is
 // aligned for it (Refill::hard_vec), else byte stores.
 template <int CPW>
-__device__ __forceinline__ void store_fin_hard(const Refill& rf, const uint64_t* __restrict__ hw, int64_t fb,
-                                               int32_t N, int32_t j0, int lane)
+__device__ __forceinline__ void store_fin_bytes(const Refill& rf, uint64_t v, int64_t fb, int32_t N, int32_t j0)
 {
-    uint64_t v = 0;
-#pragma unroll
-    for (int c = 0; c < CPW; ++c) v |= ((hw[c] >> lane) & 1ull) << (8 * c);
     uint8_t* p = rf.hard_out + (size_t)fb * N + j0;
     if (rf.hard_vec && (CPW == 8 || CPW == 4 || CPW == 2 || CPW == 1)) {
         if constexpr (CPW == 8) *reinterpret_cast<uint64_t*>(p) = v;
@@ -114,6 +110,15 @@ __device__ __forceinline__ void store_fin_hard(const Refill& rf, const uint64_t*
 #pragma unroll
         for (int c = 0; c < CPW; ++c) p[c] = (uint8_t)(v >> (8 * c));
     }
+}
+template <int CPW>
+__device__ __forceinline__ void store_fin_hard(const Refill& rf, const uint64_t* __restrict__ hw, int64_t fb,
+                                               int32_t N, int32_t j0, int lane)
+{
+    uint64_t v = 0;
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) v |= ((hw[c] >> lane) & 1ull) << (8 * c);
+    store_fin_bytes<CPW>(rf, v, fb, N, j0);
 }
 
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
@@ -129,16 +134,25 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
 // ln0 / b0: the lane's cs.lane_n / cs.lane_b, loaded by the caller (only
 // meaningful for occupied lanes).  probe: read the claim counter before
 // claiming (avoids atomics on it once the input is exhausted).
+// ffm / U0 (FirstCheck): lanes refilled at the previous step, whose first
+// check ran from their codes -- iteration 0's syndrome is U0 (Init's
+// decisions), iteration 1's is U (the ballots), evaluated in that order as
+// the reference's loop would (dec.cpp:1223-1246).
 __device__ __forceinline__ void cont_lanes(int64_t t, uint64_t occ, uint64_t U, int32_t max_iter, const ContState& cs,
                                            const ContOut& co, int64_t* s_b, int32_t* s_n, uint64_t* s_fin,
-                                           int32_t ln0, int64_t b0, bool probe)
+                                           int32_t ln0, int64_t b0, bool probe, uint64_t ffm = 0ull,
+                                           uint64_t U0 = 0ull)
 {
     const int lane = lane_id();
     {
         const size_t li = (size_t)t * TILE + lane;
         const bool o = (occ >> lane) & 1ull;
-        const int32_t ln = o ? ln0 : 0;
-        const bool unsat = (U >> lane) & 1ull;
+        int32_t ln = o ? ln0 : 0;
+        bool unsat = (U >> lane) & 1ull;
+        if ((ffm >> lane) & 1ull) {
+            if ((U0 >> lane) & 1ull) ln = 1;        // iteration 0 unsatisfied: iteration 1 decides
+            else { ln = 0; unsat = false; }         // Init's decisions are a codeword: iters 0
+        }
         const bool fin = o && (!unsat || ln == max_iter);
         const bool cont = o && !fin;
         const int64_t b = o ? b0 : -1;
@@ -202,16 +216,17 @@ __device__ __forceinline__ uint64_t row_parity(const uint64_t* __restrict__ h, c
 // lane bookkeeping for the step (cont_lanes: iters / valid, refill claims,
 // active / fresh / occupied masks) and hands the finished lanes to the
 // variable kernel, which writes their outputs before refilling them.
+// p0: the block's OR of iteration-0 row parities (FirstCheck, rs.unsat0 set).
 __device__ __forceinline__ void res_arrive(int64_t t, uint64_t occ, uint64_t p, const ResStep& rs, int32_t ln0,
-                                           int64_t b0, uint32_t nblk)
+                                           int64_t b0, uint32_t nblk, uint64_t p0 = 0ull)
 {
-    __shared__ uint64_t red[4];
+    __shared__ uint64_t red[4], red0[4];
     __shared__ int64_t s_b[TILE];
     __shared__ int32_t s_n[TILE];
     __shared__ uint64_t s_fin;
     __shared__ int s_last;
     const int lane = lane_id(), w = wave_id();
-    if (lane == 0) red[w] = p;
+    if (lane == 0) { red[w] = p; red0[w] = p0; }
     __syncthreads();
     // No fences: an agent-scope release would write back the L2 in every
     // block.  Only device-coherent atomics carry data between the blocks; the
@@ -220,22 +235,29 @@ __device__ __forceinline__ void res_arrive(int64_t t, uint64_t occ, uint64_t p, 
     // bookkeeping reads was written by earlier kernels.
     if (threadIdx.x == 0) {
         const uint64_t U = red[0] | red[1] | red[2] | red[3];
-        unsigned long long o = 0;
+        const uint64_t U0 = red0[0] | red0[1] | red0[2] | red0[3];
+        unsigned long long o = 0, o0 = 0;
         if (U) o = atomicOr(rs.unsat + t, (unsigned long long)U);
-        asm volatile("" ::"v"(o) : "memory");
+        if (U0) o0 = atomicOr(rs.unsat0 + t, (unsigned long long)U0);
+        asm volatile("" ::"v"(o), "v"(o0) : "memory");
         s_last = atomicAdd(rs.done + t, 1u) == nblk - 1;
     }
     __syncthreads();
     if (!s_last) return;
     if (threadIdx.x < TILE) {
         const uint64_t U = occ ? (uint64_t)atomicOr(rs.unsat + t, 0ull) : 0ull;
-        cont_lanes(t, occ, U, rs.max_iter, rs.cs, rs.co, s_b, s_n, &s_fin, ln0, b0, false);
+        // lanes refilled at the previous step with their first check from codes
+        // (read before cont_lanes rewrites the fresh mask)
+        const uint64_t ffm = rs.unsat0 ? (rs.cs.fresh[t] & occ) : 0ull;
+        const uint64_t U0 = ffm ? (uint64_t)atomicOr(rs.unsat0 + t, 0ull) : 0ull;
+        cont_lanes(t, occ, U, rs.max_iter, rs.cs, rs.co, s_b, s_n, &s_fin, ln0, b0, false, ffm, U0);
         const size_t li = (size_t)t * TILE + lane;
         rs.fin_b[li] = s_b[lane];
         rs.fin_n[li] = s_n[lane];
         if (lane == 0) {
             rs.fin[t] = s_fin;
             atomicExch(rs.unsat + t, 0ull);
+            if (rs.unsat0) atomicExch(rs.unsat0 + t, 0ull);
             atomicExch(rs.done + t, 0u);
         }
     }
@@ -996,19 +1018,23 @@ constexpr uint32_t MSA_META_ID = 0x7fu;      // meta bits 0-6: low bits of min1'
 constexpr uint32_t MSA_META_NONE = 0x1000u;  // meta bit 12: no min1 (never equals an edge's low bits)
 
 // grid (ceil(M/4), group tiles), block 256: one wave per (row, tile); the
-// v2c group is streamed once (NT: nontemporal loads).
-template <int DC, bool NT>
+// v2c group is streamed once (NT: nontemporal loads).  FF (FirstCheck): the
+// lanes claimed at this step's syndrome take their row's inputs from their
+// codes -- Init_MSA_INF's v2c = LLR of each column -- and their iteration-0
+// row parity goes to fc.u0_rows.
+template <int DC, bool NT, bool FF = false>
 __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, double* __restrict__ rec,
                                                      uint16_t* __restrict__ meta, const uint64_t* __restrict__ active,
-                                                     int32_t M, int64_t E, int64_t t0)
+                                                     int32_t M, int64_t E, int64_t t0, FirstCheck fc)
 {
     static_assert(DC >= 2 && DC <= 96, "row degree");
     const int lane = lane_id();
     const int32_t row = blockIdx.x * 4 + wave_id();
     const int64_t t = t0 + blockIdx.y;
     const uint64_t act = active[t];
+    const uint64_t frm = FF ? fc.fresh[t] : 0ull;
     // whole-line policy (as k_check_msa)
-    if (!(row < M && line_occupied(act, lane))) return;
+    if (!(row < M && line_occupied(act | frm, lane))) return;
     // the row's DC segments through a buffer resource: per-edge offsets in
     // the instructions, one per-lane VGPR offset (no 64-bit addresses)
     const auto rv2c = buf_rsrc(v2c + ((size_t)t * E + (size_t)row * DC) * TILE, (uint64_t)DC * TILE * 8);
@@ -1017,6 +1043,32 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     for (int k = 0; k < DC; ++k)
         x[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv2c, lane * 8, k * (TILE * 8),
                                                                                NT ? kBufNT : 0));
+    if constexpr (FF) {
+        if (frm != 0ull) {  // tile-uniform
+            // a tile's refills hold consecutive codewords (one claim per tile,
+            // cont_lanes): one buffer resource over their 64 input rows
+            const bool fr = (frm >> lane) & 1ull;
+            const int64_t bmin = fc.lane_b[t * TILE + __builtin_ctzll(frm)];
+            const int64_t bl = fr ? fc.lane_b[t * TILE + lane] : bmin;
+            const auto rin = buf_rsrc(fc.in_code + (size_t)bmin * fc.N, (uint64_t)TILE * fc.N);
+            const int voff = (int)(bl - bmin) * fc.N;
+            const int32_t* __restrict__ cols = fc.col_idx + (size_t)row * DC;  // wave-uniform: scalar loads
+            uint32_t p0 = 0;
+            if (fr) {
+                int8_t k8[DC];
+#pragma unroll
+                for (int k = 0; k < DC; ++k) k8[k] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rin, voff, cols[k], 0);
+#pragma unroll
+                for (int k = 0; k < DC; ++k) {
+                    x[k] = fc.ptab[k8[k] + kCodeBias];
+                    p0 ^= (x[k] > 0) ? 0u : 1u;  // Init_MSA_INF's decision !(LLR > 0)
+                }
+            }
+            const uint64_t pm = __ballot(fr && p0);
+            if (lane == __builtin_ctzll(__ballot(1)))
+                fc.u0_rows[(size_t)t * M + row] = pm;
+        }
+    }
     // one pass: min1 with its FIRST index, min2 = minimum over the other
     // indices (a tie with min1 gives min2 == min1), NaN never compares less
     double m1 = __builtin_inf(), m2 = __builtin_inf();
@@ -1075,8 +1127,11 @@ __device__ __forceinline__ uint32_t er_pos(uint32_t er, int DC)
 // record loads (their plane depends on the meta word), all through buffer
 // resources (per-edge offsets in SGPRs); NT: nontemporal v2c stores (the
 // group's v2c is read back once, by the next check phase).  PC: coded
-// priors, as k_var_m.
-template <int DC, int DV, bool CONT, int CPW, bool NT, bool PC = false>
+// priors, as k_var_m.  FF (FirstCheck, with CONT and PC): a refilled lane's
+// first check ran in this step's check kernel, so it runs its first update
+// here (prior = its codes' LLR, own v2c signs = the LLR's sign, as Init_MSA_INF
+// left them) instead of Init_MSA_INF's stores.
+template <int DC, int DV, bool CONT, int CPW, bool NT, bool PC = false, bool FF = false>
 __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ rec, const uint16_t* __restrict__ meta,
                                                    double* __restrict__ v2c,
                                                    double* __restrict__ prior, uint64_t* __restrict__ hard,
@@ -1114,6 +1169,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
     const auto rmeta = buf_rsrc(meta + (size_t)ty * M * TILE, (uint64_t)M * TILE * sizeof(uint16_t));
     const auto rv2c = buf_rsrc(v2c + (size_t)t * E * TILE, (uint64_t)E * TILE * sizeof(double));
     static_assert(CONT || !PC, "coded priors come with continuous refills");
+    static_assert(!FF || (CONT && PC), "first check from codes: coded continuous refills");
     double l[CPW][DV], pv[CPW], xin[CPW];
     int8_t kin[CPW];  // PC: the refilled lane's input codes
     if (fr) {
@@ -1124,7 +1180,9 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             else xin[c] = rf.in[rb + j0 + c];
         }
     }
-    if (live) {
+    // lanes updated this step: the live ones, and with FF the refilled ones
+    const bool upd = live || (FF && fr);
+    if (upd) {
         // the meta words first; from them, per edge a 4-bit code (bit 0: the
         // c2v sign = parity ^ own sign, bits 1-2: the record plane -- m2 at the
         // row's min1 edge, a NaN plane when x_0 / x_1 is NaN, else m1), packed
@@ -1135,8 +1193,13 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
         uint32_t sb[CPW], mw[CPW][DV], cpk[CPW];  // mw: the u16 meta words
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
-            pv[c] = prior_at<PC>(prior, rf, ((size_t)t * N + j0 + c) * TILE + lane);
-            sb[c] = sgn[((size_t)t * N + j0 + c) * TILE + lane];
+            if (FF && fr) {  // Init_MSA_INF's state: prior LLR, every own v2c = LLR
+                pv[c] = rf.ptab[kin[c] + kCodeBias];
+                sb[c] = (pv[c] >= 0) ? 0u : 0xffu;
+            } else {
+                pv[c] = prior_at<PC>(prior, rf, ((size_t)t * N + j0 + c) * TILE + lane);
+                sb[c] = sgn[((size_t)t * N + j0 + c) * TILE + lane];
+            }
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
                 const int rid = (int)(er[c][s] >> MSA_ER_SHIFT);
@@ -1181,11 +1244,19 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
 #pragma unroll
             for (int s = 0; s < DV; ++s) l[c][s] = flip_sign(l[c][s], cpk[c] >> (4 * s));
     }
-    if (CONT && fl) {  // finished codeword: hard bits of its exit (ballots before this step's update)
-        uint64_t hw[CPW];
+    if (CONT && fl) {
+        // finished codeword: hard bits of its exit -- the ballots before this
+        // step's update, or at iteration 0 Init_MSA_INF's decisions !(LLR > 0)
+        // (with FF the ballots already hold its first update's)
+        uint64_t v = 0;
 #pragma unroll
-        for (int c = 0; c < CPW; ++c) hw[c] = hard[(size_t)t * N + j0 + c];
-        store_fin_hard<CPW>(rf, hw, fb, N, j0, lane);
+        for (int c = 0; c < CPW; ++c) {
+            const size_t pj = ((size_t)t * N + j0 + c) * TILE + lane;
+            const bool hb = fn > 0 ? ((hard[(size_t)t * N + j0 + c] >> lane) & 1ull) != 0ull
+                                   : !(prior_at<PC>(prior, rf, pj) > 0);
+            v |= (uint64_t)hb << (8 * c);
+        }
+        store_fin_bytes<CPW>(rf, v, fb, N, j0);
     }
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
@@ -1199,12 +1270,12 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
         double dv[DV];
 #pragma unroll
         for (int s = 0; s < DV; ++s) dv[s] = 0.0;
-        if (fr) {  // Init_MSA_INF for a refilled lane
+        if (!FF && fr) {  // Init_MSA_INF for a refilled lane
             const double x = PC ? rf.ptab[kin[c] + kCodeBias] : xin[c];
 #pragma unroll
             for (int s = 0; s < DV; ++s) dv[s] = x;
             h = !(x > 0);
-        } else if (live) {
+        } else if (upd) {
             // v2c_s = LLR + c_0 + ... (skipping c_s), L = LLR + all, in the
             // reference's left-to-right order: v2c_s continues the shared
             // prefix P_s = LLR + c_0 + ... + c_{s-1} with c_{s+1} .. c_{DV-1}
@@ -1225,6 +1296,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             else prior[pj] = xin[c];
         }
         if (line_occupied(touched, lane) || fr || live) {  // whole-line stores, as k_var_m
+            // (a refilled lane's v2c: Init's copies of its LLR, or with FF its first update's)
             uint32_t sbn = 0;
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
@@ -1294,6 +1366,7 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ pos
 __global__ __launch_bounds__(256) void k_cont_reset(uint64_t* __restrict__ active, uint64_t* __restrict__ fresh,
                                                     uint64_t* __restrict__ occupied, unsigned long long* __restrict__ ctr,
                                                     int32_t nctr, unsigned long long* __restrict__ unsat,
+                                                    unsigned long long* __restrict__ unsat0,
                                                     unsigned* __restrict__ done, int64_t tiles)
 {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tiles; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1301,6 +1374,7 @@ __global__ __launch_bounds__(256) void k_cont_reset(uint64_t* __restrict__ activ
         fresh[i] = 0;
         occupied[i] = 0;
         if (unsat) unsat[i] = 0;
+        if (unsat0) unsat0[i] = 0;
         if (done) done[i] = 0;
     }
     if (blockIdx.x == 0 && (int32_t)threadIdx.x < nctr) ctr[threadIdx.x] = 0;
@@ -1323,7 +1397,10 @@ __global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs)
     const int lane = lane_id();
     int32_t ln0 = 0;
     int64_t b0 = 0;
-    uint64_t u = 0;
+    uint64_t u = 0, u0 = 0;
+    // FirstCheck: lanes refilled at the previous step; their iteration-0 row
+    // parities are in u0_rows (written by that step's check kernel)
+    const bool ff = rs.u0_rows && occ && (rs.cs.fresh[t] & occ);
     if (occ) {
         if (threadIdx.x < TILE && ((occ >> lane) & 1ull)) {
             ln0 = rs.cs.lane_n[t * TILE + lane];
@@ -1342,6 +1419,7 @@ __global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs)
                     if (k < DC) p ^= h[cols[k]];
                 }
             }
+            if (ff && part == 0 && row < M) u0 |= rs.u0_rows[(size_t)t * M + row];
             p ^= shfl_xor_u64(p, 8);
             p ^= shfl_xor_u64(p, 16);
             p ^= shfl_xor_u64(p, 32);
@@ -1350,8 +1428,12 @@ __global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs)
         u |= shfl_xor_u64(u, 1);
         u |= shfl_xor_u64(u, 2);
         u |= shfl_xor_u64(u, 4);
+        if (ff) {
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) u0 |= shfl_xor_u64(u0, off);
+        }
     }
-    res_arrive(t, occ, u, rs, ln0, b0, gridDim.x);
+    res_arrive(t, occ, u, rs, ln0, b0, gridDim.x, u0);
 }
 
 // hard ballots -> [b][N] u8 (the reference's dblk / dec_*.txt bits)

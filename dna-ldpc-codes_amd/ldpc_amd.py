@@ -132,6 +132,7 @@ EXPORTS = [
     "ldpc_abi_version", "ldpc_last_error", "ldpc_device_count", "ldpc_graph_load", "ldpc_graph_from_edges",
     "ldpc_graph_load_alist", "ldpc_graph_rs_ldpc", "ldpc_graph_save_pchk", "ldpc_graph_save_alist",
     "ldpc_graph_free", "ldpc_graph_info", "ldpc_graph_blocks", "ldpc_graph_edges", "ldpc_graph_syndrome", "ldpc_decode",
+    "ldpc_decode_codes",
     "ldpc_engine_create", "ldpc_engine_create_ex", "ldpc_engine_info", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
     "ldpc_engine_decode_codes", "ldpc_engine_gen_bsc", "ldpc_engine_gen_bsc_codes", "ldpc_engine_set_params", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
     "ldpc_dev_memcpy", "ldpc_dna_llr", "ldpc_dna_edit_distance", "ldpc_write_soft_files", "ldpc_py_float_repr",
@@ -173,6 +174,7 @@ def lib():
         L.ldpc_graph_blocks.argtypes = [vp, vp, vp, vp, vp]
         L.ldpc_graph_syndrome.argtypes = [vp, vp, vp]
         L.ldpc_decode.argtypes = [vp, vp, i64, i32, i32, vp, vp, vp, vp, C.POINTER(Opts)]
+        L.ldpc_decode_codes.argtypes = [vp, vp, vp, i32, i64, i32, i32, vp, vp, vp, vp, C.POINTER(Opts)]
         L.ldpc_engine_create.argtypes = [vp, i32, i32, i64, pint]
         L.ldpc_engine_create.restype = vp
         L.ldpc_engine_create_ex.argtypes = [vp, i32, i32, i64, C.POINTER(Schedule), pint]
@@ -348,16 +350,37 @@ class Graph:
         None.  msa_* / tie_seed: parameters of algo='qmsa' (0 = defaults q 6,
         step 0.5).  schedule: a Schedule or a dict of its keywords (None: the
         library's default schedule)."""
-        a = _algo(algo)
         x = np.ascontiguousarray(llr, dtype=np.float64)
+        return self._decode(x, "llr", None, IN_LLR, max_iter, algo, post, devices, chunk, exp_on_host, host_threads,
+                            msa_precision, msa_step, msa_offset, tie_seed, schedule)
+
+    def decode_codes(self, codes: np.ndarray, table: np.ndarray, table_kind: int = IN_LLR, max_iter: int = 200,
+                     algo="bp", post: Optional[str] = "llr", devices: Optional[Sequence[int]] = None, chunk: int = 0,
+                     host_threads: int = 0, msa_precision: int = 0, msa_step: float = 0.0, msa_offset: int = 0,
+                     tie_seed: int = 0, schedule=None):
+        """Decode a batch given as int8 codes ([B][N] or [N]) and a 256-entry
+        table (table[k + 128] = the channel LLR of code k, or with
+        table_kind=IN_LR and BP its LR) -- the DNA stage's count differences
+        with table k * ln((1-eps)/eps) (decoder.py:314), ldpc_decode_codes.
+        Same outputs as decode(table[codes + 128])."""
+        x = np.ascontiguousarray(codes, dtype=np.int8)
+        t = np.ascontiguousarray(table, dtype=np.float64)
+        if t.shape != (256,):
+            raise ValueError("the code table has 256 entries (code + 128)")
+        return self._decode(x, "codes", t, int(table_kind), max_iter, algo, post, devices, chunk, True, host_threads,
+                            msa_precision, msa_step, msa_offset, tie_seed, schedule)
+
+    def _decode(self, x, form, table, table_kind, max_iter, algo, post, devices, chunk, exp_on_host, host_threads,
+                msa_precision, msa_step, msa_offset, tie_seed, schedule):
+        a = _algo(algo)
         single = x.ndim == 1
         if single:
             x = x[None, :]
         if x.ndim != 2 or x.shape[1] != self.N:
-            raise ValueError(f"llr must have shape [B][{self.N}]")
+            raise ValueError(f"{form} must have shape [B][{self.N}]")
         B = x.shape[0]
-        hard = np.zeros((B, self.N), np.uint8)
-        postv = np.zeros((B, self.N), np.float64) if post else None
+        hard = np.empty((B, self.N), np.uint8)
+        postv = np.empty((B, self.N), np.float64) if post else None
         iters = np.zeros(B, np.int32)
         valid = np.zeros(B, np.uint8)
         o = Opts()
@@ -375,8 +398,12 @@ class Graph:
         sch = _schedule(schedule)
         if sch is not None:
             o.schedule = C.pointer(sch)
-        _check(lib().ldpc_decode(self._h, _ptr(x), B, int(max_iter), a, _ptr(hard), _ptr(postv), _ptr(iters),
-                                 _ptr(valid), C.byref(o)))
+        if form == "codes":
+            _check(lib().ldpc_decode_codes(self._h, _ptr(x), _ptr(table), table_kind, B, int(max_iter), a, _ptr(hard),
+                                           _ptr(postv), _ptr(iters), _ptr(valid), C.byref(o)))
+        else:
+            _check(lib().ldpc_decode(self._h, _ptr(x), B, int(max_iter), a, _ptr(hard), _ptr(postv), _ptr(iters),
+                                     _ptr(valid), C.byref(o)))
         valid = valid.astype(bool)
         if single:
             return hard[0], (postv[0] if postv is not None else None), int(iters[0]), bool(valid[0])

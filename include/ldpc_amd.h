@@ -210,6 +210,19 @@ int ldpc_decode(const ldpc_graph *g, const double *llr, int64_t B, int32_t max_i
                 uint8_t *hard_out, double *post_out, int32_t *iters_out, uint8_t *valid_out,
                 const ldpc_opts *opts);
 
+/* The same decode for a channel output held as small integers -- the DNA
+ * pipeline's per-bit read-count differences k = count_0 - count_1, whose LLR
+ * is k * ln((1-eps)/eps) (decoder.py:314) -- so no [B][N] fp64 matrix is
+ * built, scanned or sent: codes [B][N] int8 (host), table[256] the channel
+ * value of code k at table[k + 128], of kind table_kind (LDPC_IN_LLR; for BP
+ * also LDPC_IN_LR).  BP's LR is the host libm exp of an LLR table entry, as
+ * DNA_main.cpp:1344 computes it per bit.  Identical results to ldpc_decode on
+ * llr[b][j] = table[codes[b][j] + 128] (LDPC_IN_LLR); one byte per bit
+ * crosses PCIe.  Outputs and opts as ldpc_decode. */
+int ldpc_decode_codes(const ldpc_graph *g, const int8_t *codes, const double *table, int32_t table_kind,
+                      int64_t B, int32_t max_iter, int32_t algo, uint8_t *hard_out, double *post_out,
+                      int32_t *iters_out, uint8_t *valid_out, const ldpc_opts *opts);
+
 /* ------------------------------------------------------------------------ */
 /* Device-resident engine (benchmarks, pipelines that keep data in HBM)      */
 /* ------------------------------------------------------------------------ */

@@ -201,3 +201,76 @@ def test_host_api_negative_zero_and_off_lattice(G, og, codewords, algo):
         h, p, it, v = G.decode(case, max_iter=mi, algo=algo, post="ratio" if a == 0 else "llr")
         assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h)
         assert np.array_equal(p.view(np.uint64), ref_p.view(np.uint64))
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("max_iter", [1, 2, 50])
+def test_msa_first_check_from_codes(gpu, G, og, codewords, max_iter):
+    """Compressed min-sum on coded input runs every refill's first check from
+    its codes in the step that claims it (dev::FirstCheck), evaluating
+    iterations 0 and 1 together at the next syndrome.  Over several pool fills
+    (2500 codewords through the 1024-lane pool, so refills land in tiles with
+    live lanes), with noiseless rows (iteration-0 exits: outputs from Init's
+    decisions) and max_iter 1 / 2 / 50: identical hard bits, posterior,
+    iterations and valid flags to the same engine kind with an Init step
+    (first_from_prior off), and a sample equal to the oracle."""
+    L = gpu
+    N, B = G.N, 2500
+    llr = synth.bsc_llrs(codewords, 0, B, seed=77, p=0.002)
+    llr[::7] = np.where(codewords[np.arange(0, B, 7) % 272] == 1, -synth.LLR_UNIT, synth.LLR_UNIT)
+    k = np.rint(llr / synth.LLR_UNIT).astype(np.int8)
+    codes = L.DeviceBuffer(0, B * N)
+    codes.upload(k)
+    outs = []
+    for ffp in (True, False):
+        eng = L.Engine(G, 0, "msa", first_from_prior=ffp)
+        assert eng.msa_compressed and eng.continuous and eng.first_from_prior == ffp
+        outs.append(_run(L, eng, B, N, lambda h, pp, it, v: eng.decode_codes(
+            codes.at(0), _table(), L.IN_LLR, B, max_iter, h, pp, L.POST_LLR, it, v)))
+        eng.close()
+    _same(outs[0], outs[1])
+    it = outs[0][2]
+    assert (it[::7] == 0).all() and outs[0][3][::7].all()
+    if max_iter == 50:
+        assert len(np.unique(it)) > 5
+    idx = np.unique(np.concatenate([np.arange(0, 21), np.arange(B - 20, B), np.arange(1000, 1030)]))
+    rh, rp, rit, rv = og.decode_batch(llr[idx], max_iter, algo=1, post_mode=0, threads=8)
+    a = outs[0]
+    assert np.array_equal(a[0][idx], rh) and np.array_equal(a[2][idx], rit) and np.array_equal(a[3][idx], rv)
+    assert np.array_equal(a[1][idx].view(np.uint64), rp.view(np.uint64))
+
+
+@pytest.mark.parametrize("algo,kw", [("bp", {}), ("bp", dict(chunk=64, devices=[0, 0])), ("msa", {}),
+                                     ("qmsa", {}), ("gallager_b1", {})])
+def test_host_decode_codes_equals_llr_decode(G, og, codewords, algo, kw):
+    """ldpc_decode_codes (the DNA stage's count differences k + the table
+    k * ln49, no fp64 matrix) == ldpc_decode on the LLRs table[k + 128], bit
+    for bit -- one fill, several chunks and devices, every decoder family --
+    and BP also equals the oracle and the LR-table form."""
+    llr = synth.dna_like_llrs(codewords, seed=21, reads=58000)[:200]
+    k = np.rint(llr / synth.LLR_UNIT).astype(np.int8)
+    assert np.array_equal(k * synth.LLR_UNIT, llr)
+    post = "ratio" if algo == "bp" else "llr"
+    a = G.decode_codes(k, _table(), max_iter=60, algo=algo, post=post, **kw)
+    b = G.decode(llr, max_iter=60, algo=algo, post=post, schedule=dict(lr_table=False), **kw)
+    for x, y in zip(a, b):
+        assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+    if algo == "bp":
+        rh, rp, rit, rv = og.decode_batch(llr, 60, algo=0, post_mode=1, threads=8)
+        assert np.array_equal(a[0], rh) and np.array_equal(a[2], rit) and np.array_equal(a[3], rv.astype(bool))
+        assert np.array_equal(a[1].view(np.uint64), rp.view(np.uint64))
+        import ldpc_amd as L
+        c = G.decode_codes(k, np.exp(_table()), table_kind=L.IN_LR, max_iter=60, post=post, **kw)
+        for x, y in zip(a, c):
+            assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+
+
+def test_host_decode_codes_errors(G):
+    import ldpc_amd as L
+    k = np.zeros((3, G.N), np.int8)
+    with pytest.raises(L.LdpcError):
+        G.decode_codes(k, np.exp(_table()), table_kind=L.IN_LR, algo="msa", max_iter=5)
+    with pytest.raises(ValueError):
+        G.decode_codes(k, _table()[:100], max_iter=5)
+    h, p, it, v = G.decode_codes(k[0], _table(), max_iter=5, post=None)  # 1-D: one codeword
+    assert h.shape == (G.N,) and p is None
