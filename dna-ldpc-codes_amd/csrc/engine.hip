@@ -452,15 +452,17 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
         return LDPC_OK;
     }
     if (msa_c) {
-        const FirstCheck fc = fcheck ? *fcheck : FirstCheck{};
-#define CHECK_MSA_C(NT, FF)                                                                                       \
-    LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, NT, FF>), grid, blk, 0, s, v2c, msa_rec(scratch),          \
-                                  msa_meta(scratch, c2v_tiles, M), active, M, E, t0, fc))
-        if (nt_d && fcheck) CHECK_MSA_C(true, true);
-        else if (nt_d) CHECK_MSA_C(true, false);
-        else if (fcheck) CHECK_MSA_C(false, true);
-        else CHECK_MSA_C(false, false);
-#undef CHECK_MSA_C
+        if (nt_d)
+            LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, true>), grid, blk, 0, s, v2c, msa_rec(scratch),
+                                          msa_meta(scratch, c2v_tiles, M), active, M, E, t0));
+        else
+            LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, false>), grid, blk, 0, s, v2c, msa_rec(scratch),
+                                          msa_meta(scratch, c2v_tiles, M), active, M, E, t0));
+        // first check of this step's refills from their codes (class "init":
+        // it stands in for Init_MSA_INF's step)
+        if (fcheck)
+            LAUNCH_ON(s, K_INIT, klaunch((k_check_msa_c_first<72>), grid, blk, 0, s, msa_rec(scratch),
+                                         msa_meta(scratch, c2v_tiles, M), M, t0, *fcheck));
         return LDPC_OK;
     }
     if (reg72) {

@@ -1018,23 +1018,19 @@ constexpr uint32_t MSA_META_ID = 0x7fu;      // meta bits 0-6: low bits of min1'
 constexpr uint32_t MSA_META_NONE = 0x1000u;  // meta bit 12: no min1 (never equals an edge's low bits)
 
 // grid (ceil(M/4), group tiles), block 256: one wave per (row, tile); the
-// v2c group is streamed once (NT: nontemporal loads).  FF (FirstCheck): the
-// lanes claimed at this step's syndrome take their row's inputs from their
-// codes -- Init_MSA_INF's v2c = LLR of each column -- and their iteration-0
-// row parity goes to fc.u0_rows.
-template <int DC, bool NT, bool FF = false>
+// v2c group is streamed once (NT: nontemporal loads).
+template <int DC, bool NT>
 __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, double* __restrict__ rec,
                                                      uint16_t* __restrict__ meta, const uint64_t* __restrict__ active,
-                                                     int32_t M, int64_t E, int64_t t0, FirstCheck fc)
+                                                     int32_t M, int64_t E, int64_t t0)
 {
     static_assert(DC >= 2 && DC <= 96, "row degree");
     const int lane = lane_id();
     const int32_t row = blockIdx.x * 4 + wave_id();
     const int64_t t = t0 + blockIdx.y;
     const uint64_t act = active[t];
-    const uint64_t frm = FF ? fc.fresh[t] : 0ull;
     // whole-line policy (as k_check_msa)
-    if (!(row < M && line_occupied(act | frm, lane))) return;
+    if (!(row < M && line_occupied(act, lane))) return;
     // the row's DC segments through a buffer resource: per-edge offsets in
     // the instructions, one per-lane VGPR offset (no 64-bit addresses)
     const auto rv2c = buf_rsrc(v2c + ((size_t)t * E + (size_t)row * DC) * TILE, (uint64_t)DC * TILE * 8);
@@ -1043,32 +1039,6 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     for (int k = 0; k < DC; ++k)
         x[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv2c, lane * 8, k * (TILE * 8),
                                                                                NT ? kBufNT : 0));
-    if constexpr (FF) {
-        if (frm != 0ull) {  // tile-uniform
-            // a tile's refills hold consecutive codewords (one claim per tile,
-            // cont_lanes): one buffer resource over their 64 input rows
-            const bool fr = (frm >> lane) & 1ull;
-            const int64_t bmin = fc.lane_b[t * TILE + __builtin_ctzll(frm)];
-            const int64_t bl = fr ? fc.lane_b[t * TILE + lane] : bmin;
-            const auto rin = buf_rsrc(fc.in_code + (size_t)bmin * fc.N, (uint64_t)TILE * fc.N);
-            const int voff = (int)(bl - bmin) * fc.N;
-            const int32_t* __restrict__ cols = fc.col_idx + (size_t)row * DC;  // wave-uniform: scalar loads
-            uint32_t p0 = 0;
-            if (fr) {
-                int8_t k8[DC];
-#pragma unroll
-                for (int k = 0; k < DC; ++k) k8[k] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rin, voff, cols[k], 0);
-#pragma unroll
-                for (int k = 0; k < DC; ++k) {
-                    x[k] = fc.ptab[k8[k] + kCodeBias];
-                    p0 ^= (x[k] > 0) ? 0u : 1u;  // Init_MSA_INF's decision !(LLR > 0)
-                }
-            }
-            const uint64_t pm = __ballot(fr && p0);
-            if (lane == __builtin_ctzll(__ballot(1)))
-                fc.u0_rows[(size_t)t * M + row] = pm;
-        }
-    }
     // one pass: min1 with its FIRST index, min2 = minimum over the other
     // indices (a tie with min1 gives min2 == min1), NaN never compares less
     double m1 = __builtin_inf(), m2 = __builtin_inf();
@@ -1099,6 +1069,83 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     meta[((size_t)blockIdx.y * M + row) * TILE + lane] =
         (uint16_t)((neg << 15) | ((nan1 ? 1u : 0u) << 14) | ((nan0 ? 1u : 0u) << 13) |
                    (i1 < 0 ? MSA_META_NONE : ((uint32_t)(row * DC + i1) & MSA_META_ID)));
+}
+
+// First check from codes (FirstCheck), after k_check_msa_c on the same
+// group: the records of the lanes claimed at this step's syndrome, from their
+// input codes -- Init_MSA_INF (dec.cpp:1300-1329) sets every v2c of column j
+// to LLR_j, so row r's inputs are its columns' LLRs -- with k_check_msa_c's
+// arithmetic (one pass: min1 with its first index, min2 over the others, the
+// sign parity of !(x >= 0), the NaN planes of x_0 / x_1), and the parity of
+// Init's decisions !(LLR > 0) over the row (the iteration-0 syndrome,
+// dec.cpp:1223) into fc.u0_rows.  Only the refilled lanes run (k_check_msa_c
+// skips lines with no live lane and writes garbage records for refilled lanes
+// in lines with one); a separate launch keeps the byte gathers and table
+// lookups off the streaming kernel's critical path.  grid (ceil(M/4), group
+// tiles), block 256; the table in LDS.
+template <int DC>
+__global__ __launch_bounds__(256) void k_check_msa_c_first(double* __restrict__ rec, uint16_t* __restrict__ meta,
+                                                           int32_t M, int64_t t0, FirstCheck fc)
+{
+    __shared__ double tab[256];
+    const int64_t t = t0 + blockIdx.y;
+    const uint64_t frm = fc.fresh[t];
+    if (frm == 0ull) return;  // block-uniform
+    tab[threadIdx.x] = fc.ptab[threadIdx.x];
+    __syncthreads();
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    if (row >= M) return;
+    const bool fr = (frm >> lane) & 1ull;
+    uint32_t p0 = 0;
+    if (fr) {
+        // a tile's refills hold consecutive codewords (one claim per tile,
+        // cont_lanes): one buffer resource over their input rows
+        const int64_t bmin = fc.lane_b[t * TILE + __builtin_ctzll(frm)];
+        const int64_t bl = fc.lane_b[t * TILE + lane];
+        const auto rin = buf_rsrc(fc.in_code + (size_t)bmin * fc.N, (uint64_t)TILE * fc.N);
+        const int voff = (int)(bl - bmin) * fc.N;
+        const int32_t* __restrict__ cols = fc.col_idx + (size_t)row * DC;  // wave-uniform: scalar loads
+        double m1 = __builtin_inf(), m2 = __builtin_inf(), a0 = 0.0, a1 = 0.0;
+        int i1 = -1;
+        uint32_t neg = 0;
+        // chunks of CH gathers in flight (all DC at once would hold DC
+        // registers and halve the occupancy that hides their latency)
+        constexpr int CH = 24;
+#pragma unroll 1
+        for (int k0 = 0; k0 < DC; k0 += CH) {
+            int32_t k8[CH];
+#pragma unroll
+            for (int i = 0; i < CH; ++i)
+                if (k0 + i < DC) k8[i] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rin, voff, cols[k0 + i], 0);
+#pragma unroll
+            for (int i = 0; i < CH; ++i) {
+                const int k = k0 + i;
+                if (k >= DC) break;
+                const double x = tab[k8[i] + kCodeBias];
+                const double a = __builtin_fabs(x);
+                if (k == 0) a0 = a;
+                if (k == 1) a1 = a;
+                neg ^= (x >= 0) ? 0u : 1u;
+                p0 ^= (x > 0) ? 0u : 1u;  // Init_MSA_INF's decision !(LLR > 0)
+                const bool lt1 = a < m1, lt2 = a < m2;
+                m2 = lt1 ? m1 : (lt2 ? a : m2);
+                m1 = lt1 ? a : m1;
+                i1 = lt1 ? k : i1;
+            }
+        }
+        const bool nan0 = __builtin_isnan(a0), nan1 = __builtin_isnan(a1);
+        double* __restrict__ r = rec + ((size_t)blockIdx.y * M + row) * (MSA_REC_PLANES * TILE) + lane;
+        r[0] = m1;
+        r[TILE] = m2;
+        if (nan0) r[2 * TILE] = a0;
+        if (nan1) r[3 * TILE] = a1;
+        meta[((size_t)blockIdx.y * M + row) * TILE + lane] =
+            (uint16_t)((neg << 15) | ((nan1 ? 1u : 0u) << 14) | ((nan0 ? 1u : 0u) << 13) |
+                       (i1 < 0 ? MSA_META_NONE : ((uint32_t)(row * DC + i1) & MSA_META_ID)));
+    }
+    const uint64_t pm = __ballot(fr && p0 != 0u);
+    if (lane == 0) fc.u0_rows[(size_t)t * M + row] = pm;
 }
 
 __device__ __forceinline__ double flip_sign(double v, uint32_t neg)
