@@ -198,7 +198,7 @@ def cpu_baseline(args, og, llr_fn, B, gpu_out, cpus):
 def kernel_names(eng, algo, coded=False, cpw=None) -> dict:
     """Template instantiations of the check / variable kernels an engine
     launches (csrc/engine.hip launch_check / launch_var), as rocprofv3 names
-    them (tools/pmc_r3.py short form); the variable kernels' last argument is
+    them (tools/pmc_summary.py short form); the variable kernels' last argument is
     PC, coded priors (coded input on a continuous schedule)."""
     msa = "true" if algo == "msa" else "false"
     pc = str(bool(coded) and eng.continuous).lower()

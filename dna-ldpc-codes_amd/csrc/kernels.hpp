@@ -1229,6 +1229,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
     }
     // lanes updated this step: the live ones, and with FF the refilled ones
     const bool upd = live || (FF && fr);
+    uint32_t cpk[CPW];  // per edge: c2v sign (bit 0) and record plane (bits 1-2), 4 bits each
     if (upd) {
         // the meta words first; from them, per edge a 4-bit code (bit 0: the
         // c2v sign = parity ^ own sign, bits 1-2: the record plane -- m2 at the
@@ -1237,7 +1238,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
         // lane needs: the wave fetches the m1 plane's lines plus only the m2
         // lines holding a lane that needs them
         constexpr int PB = TILE * 8;  // bytes per record plane of one row
-        uint32_t sb[CPW], mw[CPW][DV], cpk[CPW];  // mw: the u16 meta words
+        uint32_t sb[CPW], mw[CPW][DV];  // mw: the u16 meta words
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             if (FF && fr) {  // Init_MSA_INF's state: prior LLR, every own v2c = LLR
@@ -1286,6 +1287,16 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
                 l[c][s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
                                                          rrec, lane * 8 + sp * PB, rid * (MSA_REC_PLANES * PB), 0));
             }
+    }
+    // a refill's prior value: its table lookup goes out behind the record
+    // loads (waiting only for its code), so the two latencies overlap
+    if constexpr (PC && !FF) {
+        if (fr) {
+#pragma unroll
+            for (int c = 0; c < CPW; ++c) xin[c] = rf.ptab[kin[c] + kCodeBias];
+        }
+    }
+    if (upd) {
 #pragma unroll
         for (int c = 0; c < CPW; ++c)
 #pragma unroll
@@ -1318,7 +1329,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
 #pragma unroll
         for (int s = 0; s < DV; ++s) dv[s] = 0.0;
         if (!FF && fr) {  // Init_MSA_INF for a refilled lane
-            const double x = PC ? rf.ptab[kin[c] + kCodeBias] : xin[c];
+            const double x = xin[c];
 #pragma unroll
             for (int s = 0; s < DV; ++s) dv[s] = x;
             h = !(x > 0);

@@ -3,7 +3,7 @@
 # bench line (as the driver runs it: --steps 20 --warmup 5), and a rocprofv3
 # kernel trace of the default bench command.  Each step under its own limit.
 set -u
-TAG=${1:-r3final}
+TAG=${1:-final}
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out/$TAG; mkdir -p "$OUT"; cd "$R"; export TMPDIR=/tmp
 run() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; tail -n 4 "$OUT/$name.log" | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi; }
 run pytest_all 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=30

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-3 measurement session: selected GPU tests, the default bench line
+# Measurement session: selected GPU tests, the default bench line
 # (with its secondary legs), rocprofv3 kernel-trace stats of the config-5
 # bench, and one PMC pass per counter group on a 16 384-codeword config-5
-# decode (tools/pmc_r3.py summarises them).  Each step has its own limit.
-#   usage: [AB="<ab_engines.py args>"] tools/gpu_r3_prof.sh <tag> [pytest -k expression ("" = skip)] [msa|bp|both|none]
+# decode (tools/pmc_summary.py summarises them).  Each step has its own limit.
+#   usage: [AB="<ab_engines.py args>"] tools/gpu_prof.sh <tag> [pytest -k expression ("" = skip)] [msa|bp|both|none]
 set -u
-TAG=${1:-r3prof}
+TAG=${1:-prof}
 K=${2-"config4 or two_rank"}
 WHICH=${3:-msa}
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out/$TAG; mkdir -p "$OUT"; cd "$R"; export TMPDIR=/tmp

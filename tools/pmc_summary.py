@@ -3,11 +3,11 @@
 group, each a run of the same bench.py command), keyed by the kernel's full
 template instantiation.
 
-    python tools/pmc_r3.py <dir with pmc_*/run_counter_collection.csv> <bench .out> [out.json]
+    python tools/pmc_summary.py <dir with pmc_*/run_counter_collection.csv> <bench .out> [out.json]
 
 To feed bench.py's roofline.traffic, merge the "per_cw_iter_by_instantiation"
 maps of the BP and min-sum summaries into profiles/r<N>/pmc_traffic.json
-(tools/pmc_r3.py --merge out.json a.json b.json ...).
+(tools/pmc_summary.py --merge out.json a.json b.json ...).
 
 <bench .out> is the stdout of one of the passes (the bench JSON line): its
 config gives the executed codeword-iterations (batch x mean_iters x steps).
