@@ -91,7 +91,7 @@ def parse():
                     help="resident in-place pool of a few tiles (-1: engine default; BP / fp64 min-sum, continuous)")
     ap.add_argument("--var-cpw", type=int, default=0, help="columns per variable-phase wave (0: engine default 4)")
     ap.add_argument("--ffp", type=int, default=-1,
-                    help="first check from the prior / codes (LDPC_SCHED_FIRST_FROM_PRIOR; -1: engine default)")
+                    help="single-fill BP: first check from the prior (LDPC_SCHED_FIRST_FROM_PRIOR; -1: engine default)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
     ap.add_argument("--secondary", type=int, default=1,
                     help="N = 1: also time config 2 (DNA batch, host API) and config 5 (1M min-sum) after the headline")
@@ -501,7 +501,7 @@ def msa_1m(args, og, threads, cw, d_cw):
     G = L.Graph(synth.PCHK)
     N = G.N
     B, p, max_iter = args.msa_batch, 0.002, 50
-    eng = L.Engine(G, 0, "msa", first_from_prior=None if args.ffp < 0 else bool(args.ffp))
+    eng = L.Engine(G, 0, "msa")
     d_in, decode = channel(L, eng, args, 0, N, 0, B, d_cw, cw.shape[0], p, L.IN_LLR)
     d_hard, d_iters, d_valid = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
 
@@ -525,7 +525,6 @@ def msa_1m(args, og, threads, cw, d_cw):
            "value": round(B * steps / el, 1), "unit": "codewords/s", "ms_per_step": round(el / steps * 1e3, 2),
            "mean_iters": round(float(iters.mean()), 3), "valid_frac": round(float(valid.mean()), 5),
            "resident_per_pass": eng.cap, "group_tiles": eng.group_tiles, "compressed_msa": eng.msa_compressed,
-           "first_check_from_codes": bool(eng.msa_compressed and eng.first_from_prior and args.input == "code"),
            "roofline": roofline(eng, G, st, cw_iters, args.input == "code")}
     if og is not None:
         n = max(8, 4 * threads)

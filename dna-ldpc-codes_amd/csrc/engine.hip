@@ -124,7 +124,6 @@ Engine::~Engine()
     if (h_poll) hipHostFree(h_poll);
     hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge); hipFree(d_col_er);
     hipFree(d_unsat); hipFree(d_done); hipFree(d_fin); hipFree(d_fin_b); hipFree(d_fin_n);
-    hipFree(d_u0rows); hipFree(d_unsat0);
     hipFree(d_sgn);
     hipFree(v2c); if (c2v != v2c) hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
     hipFree(post_t);
@@ -247,10 +246,6 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         LDPC_HIP(hipMalloc((void**)&d_fin, (size_t)cap_tiles * sizeof(uint64_t)));
         LDPC_HIP(hipMalloc((void**)&d_fin_b, (size_t)cap * sizeof(int64_t)));
         LDPC_HIP(hipMalloc((void**)&d_fin_n, (size_t)cap * sizeof(int32_t)));
-        if (msa_c && sched_flag(sched, LDPC_SCHED_FIRST_FROM_PRIOR)) {
-            LDPC_HIP(hipMalloc((void**)&d_u0rows, (size_t)cap_tiles * g->M * sizeof(uint64_t)));
-            LDPC_HIP(hipMalloc((void**)&d_unsat0, (size_t)cap_tiles * sizeof(unsigned long long)));
-        }
         // grouped continuous schedule: a separate syndrome launch spread over
         // several blocks per tile (the resident pool fuses it into the check)
         syn_blocks = res ? 0 : sched.syn_blocks;
@@ -283,8 +278,7 @@ int32_t Engine::flags() const
 {
     return (nt_d ? LDPC_SCHED_NONTEMPORAL : 0) | (cont ? LDPC_SCHED_CONTINUOUS : 0) |
            (msa_c ? LDPC_SCHED_MSA_COMPRESSED : 0) | (res ? LDPC_SCHED_RESIDENT : 0) |
-           (syn_blocks > 0 ? LDPC_SCHED_SPLIT_SYNDROME : 0) |
-           ((first_fp || d_u0rows) ? LDPC_SCHED_FIRST_FROM_PRIOR : 0) |
+           (syn_blocks > 0 ? LDPC_SCHED_SPLIT_SYNDROME : 0) | (first_fp ? LDPC_SCHED_FIRST_FROM_PRIOR : 0) |
            (sched.flags & (LDPC_SCHED_LR_TABLE | LDPC_SCHED_DEBUG_NO_DRAIN));
 }
 
@@ -458,11 +452,6 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
         else
             LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, false>), grid, blk, 0, s, v2c, msa_rec(scratch),
                                           msa_meta(scratch, c2v_tiles, M), active, M, E, t0));
-        // first check of this step's refills from their codes (class "init":
-        // it stands in for Init_MSA_INF's step)
-        if (fcheck)
-            LAUNCH_ON(s, K_INIT, klaunch((k_check_msa_c_first<72>), grid, blk, 0, s, msa_rec(scratch),
-                                         msa_meta(scratch, c2v_tiles, M), M, t0, *fcheck));
         return LDPC_OK;
     }
     if (reg72) {
@@ -540,14 +529,13 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         const unsigned nb = gt * (unsigned)(N / (4 * cpw));
         const double* rec = msa_rec(scratch);
         const uint16_t* meta = msa_meta(scratch, c2v_tiles, M);
-#define VAR_MSA_C3(CONT, CPW, NT, PC, FF)                                                                       \
-    klaunch((k_var_msa_c<72, 8, CONT, CPW, NT, PC, FF>), dim3(nb), dim3(256), 0, s, rec, meta, v2c, prior, hard, \
-            d_sgn, active, d_col_er, pt, N, M, E, t0, (uint32_t)gt, rf)
-#define VAR_MSA_C2(CONT, CPW, NT)                                                 \
-    do {                                                                          \
-        if (CONT && rf.in_code && rf.ff) VAR_MSA_C3(CONT, CPW, NT, CONT, CONT);   \
-        else if (CONT && rf.in_code) VAR_MSA_C3(CONT, CPW, NT, CONT, false);      \
-        else VAR_MSA_C3(CONT, CPW, NT, false, false);                             \
+#define VAR_MSA_C3(CONT, CPW, NT, PC)                                                                                \
+    klaunch((k_var_msa_c<72, 8, CONT, CPW, NT, PC>), dim3(nb), dim3(256), 0, s, rec, meta, v2c, prior, hard, d_sgn, \
+            active, d_col_er, pt, N, M, E, t0, (uint32_t)gt, rf)
+#define VAR_MSA_C2(CONT, CPW, NT)                                   \
+    do {                                                            \
+        if (CONT && rf.in_code) VAR_MSA_C3(CONT, CPW, NT, CONT);    \
+        else VAR_MSA_C3(CONT, CPW, NT, false);                      \
     } while (0)
 #define VAR_MSA_C(CONT, CPW)              \
     do {                                  \
@@ -879,27 +867,12 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     double* pt = d_post ? post_t : nullptr;
     // lane masks, claim counter + occupancy ring and the syndrome words in one launch
     static_assert(1 + kRing <= 256, "occupancy ring");
-    // compressed min-sum on coded input: every refill's first check from its
-    // codes in the step that claims it (dev::FirstCheck), no Init step
-    const bool ff = msa_c && cur_codes && d_u0rows && max_iter >= 1;
     LAUNCH(K_OTHER, klaunch(k_cont_reset, dim3((unsigned)std::min<int64_t>((tiles + 255) / 256, 1024)), dim3(256), 0,
-                            stream, active, d_fresh, d_occ, d_ctr, 1 + kRing, d_unsat, ff ? d_unsat0 : nullptr,
-                            d_done, tiles));
+                            stream, active, d_fresh, d_occ, d_ctr, 1 + kRing, d_unsat, d_done, tiles));
     ContState cs{active, d_fresh, d_occ, d_lane_b, d_lane_n, d_ctr, nullptr, B};
     cs.ntiles = tiles;
     const uint64_t q0 = poll_seq;  // this decode's first poll
     ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, ContOut{d_iters, d_valid}};
-    FirstCheck fc{};
-    if (ff) {
-        rs.u0_rows = d_u0rows;
-        rs.unsat0 = d_unsat0;
-        fc = FirstCheck{d_fresh, d_lane_b, cur_codes, d_ptab, d_col_idx, d_u0rows, N};
-    }
-    struct Unset {
-        const FirstCheck** p;
-        ~Unset() { *p = nullptr; }
-    } unset{&fcheck};
-    fcheck = ff ? &fc : nullptr;
     const int hard_vec = ((uintptr_t)d_hard % 8 == 0 && N % 8 == 0) ? 1 : 0;
     Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
               d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
@@ -908,7 +881,6 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         rf.in_code = cur_codes;
         rf.pcode = pcode;
         rf.ptab = d_ptab;
-        rf.ff = ff ? 1 : 0;
     }
     // A batch that fits the lane pool in one fill (the DNA batch) polls one
     // step behind instead of kLag: its steps take >= 30 us, time enough to
@@ -991,10 +963,9 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                 else
                     LAUNCH(K_CHECK, klaunch((k_check_bp_first<72>), dim3((M + 3) / 4, gt), dim3(256), 0, stream,
                                             prior, pcode, d_ptab, d_col_idx, c2v, active, M, N, (int64_t)g->E, t0));
-            } else if (s == 0 && !ff) {
+            } else if (s == 0) {
                 // step 0: the reset left every lane empty and the syndrome
                 // launch above only claims codewords, so no lane is active
-                // (with FirstCheck the claimed lanes' first check runs)
             } else if ((rc = launch_check(stream, c2v, t0, gt))) {
                 return rc;
             }

@@ -63,12 +63,6 @@ struct Engine {
     int64_t* d_fin_b = nullptr;             // [tile*64] their codeword index
     int32_t* d_fin_n = nullptr;             // [tile*64] their iteration count
     const dev::ResStep* rstep = nullptr;    // res: set around the check launch of a step
-    // first check from codes (compressed min-sum, coded input; dev::FirstCheck):
-    // iteration-0 row parities of the lanes refilled at a step and their
-    // per-tile OR; fcheck is set around run_cont's steps when in use
-    uint64_t* d_u0rows = nullptr;           // [tile][M]
-    unsigned long long* d_unsat0 = nullptr; // [tile]
-    const dev::FirstCheck* fcheck = nullptr;
     static constexpr int kRing = 8, kLag = 2;
     uint64_t* d_fresh = nullptr;
     uint64_t* d_occ = nullptr;

@@ -33,30 +33,6 @@ struct Refill {
     const int8_t* in_code = nullptr;
     int8_t* pcode = nullptr;
     const double* ptab = nullptr;
-    // first check from codes (compressed min-sum, coded input): a refilled
-    // lane's first check ran in this step's check kernel straight from its
-    // input codes (FirstCheck), so the variable kernel runs its first
-    // iteration's update instead of Init_MSA_INF's stores
-    int ff = 0;
-};
-
-// First check from codes (compressed min-sum with coded input, every refill):
-// the check kernel of the step that claims a codeword computes its first
-// check phase from the input codes -- Init_MSA_INF (dec.cpp:1300-1329) sets
-// every v2c of column j to LLR_j, so row r's messages are the LLRs of its
-// columns -- instead of spending a step on storing E copies of them.  The
-// iteration-0 syndrome (the parity of !(LLR > 0) over each row, dec.cpp:1223
-// on Init's decisions) is taken in the same pass: u0_rows[t][row] gets the
-// ballot of the refilled lanes whose row parity is 1, and the next step's
-// syndrome ORs it into the tile's iteration-0 word.
-struct FirstCheck {
-    const uint64_t* fresh = nullptr;  // [tile] lanes claimed at this step's syndrome
-    const int64_t* lane_b = nullptr;  // [tile*64] their codeword index
-    const int8_t* in_code = nullptr;  // [B][N] input codes
-    const double* ptab = nullptr;     // [256] LLR of code k at k + 128
-    const int32_t* col_idx = nullptr; // [E] CSR column of each edge
-    uint64_t* u0_rows = nullptr;      // [tile][M] iteration-0 row parities of the refilled lanes
-    int32_t N = 0;
 };
 
 // prior value of a code (coded input): table indexed by code + 128
@@ -107,12 +83,6 @@ struct ResStep {
     int32_t N, max_iter;
     ContState cs;
     ContOut co;                  // iters / valid (hard / post are written by the variable kernel)
-    // first check from codes (FirstCheck): the lanes refilled at the previous
-    // step are evaluated for iterations 0 and 1 at once -- iteration 0's
-    // syndrome from u0_rows (OR-reduced into unsat0, re-armed by the last
-    // block), iteration 1's from the ballots
-    const uint64_t* u0_rows = nullptr;  // [tile][M]
-    unsigned long long* unsat0 = nullptr;  // [tile]
 };
 
 }  // namespace dev

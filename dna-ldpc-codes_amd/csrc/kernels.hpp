@@ -98,8 +98,12 @@ __device__ __forceinline__ bool line_occupied(uint64_t m, int lane)
 // (pre-update ballots), one CPW-byte store per lane when the output is
 // aligned for it (Refill::hard_vec), else byte stores.
 template <int CPW>
-__device__ __forceinline__ void store_fin_bytes(const Refill& rf, uint64_t v, int64_t fb, int32_t N, int32_t j0)
+__device__ __forceinline__ void store_fin_hard(const Refill& rf, const uint64_t* __restrict__ hw, int64_t fb,
+                                               int32_t N, int32_t j0, int lane)
 {
+    uint64_t v = 0;
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) v |= ((hw[c] >> lane) & 1ull) << (8 * c);
     uint8_t* p = rf.hard_out + (size_t)fb * N + j0;
     if (rf.hard_vec && (CPW == 8 || CPW == 4 || CPW == 2 || CPW == 1)) {
         if constexpr (CPW == 8) *reinterpret_cast<uint64_t*>(p) = v;
@@ -110,15 +114,6 @@ __device__ __forceinline__ void store_fin_bytes(const Refill& rf, uint64_t v, in
 #pragma unroll
         for (int c = 0; c < CPW; ++c) p[c] = (uint8_t)(v >> (8 * c));
     }
-}
-template <int CPW>
-__device__ __forceinline__ void store_fin_hard(const Refill& rf, const uint64_t* __restrict__ hw, int64_t fb,
-                                               int32_t N, int32_t j0, int lane)
-{
-    uint64_t v = 0;
-#pragma unroll
-    for (int c = 0; c < CPW; ++c) v |= ((hw[c] >> lane) & 1ull) << (8 * c);
-    store_fin_bytes<CPW>(rf, v, fb, N, j0);
 }
 
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
@@ -134,25 +129,16 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
 // ln0 / b0: the lane's cs.lane_n / cs.lane_b, loaded by the caller (only
 // meaningful for occupied lanes).  probe: read the claim counter before
 // claiming (avoids atomics on it once the input is exhausted).
-// ffm / U0 (FirstCheck): lanes refilled at the previous step, whose first
-// check ran from their codes -- iteration 0's syndrome is U0 (Init's
-// decisions), iteration 1's is U (the ballots), evaluated in that order as
-// the reference's loop would (dec.cpp:1223-1246).
 __device__ __forceinline__ void cont_lanes(int64_t t, uint64_t occ, uint64_t U, int32_t max_iter, const ContState& cs,
                                            const ContOut& co, int64_t* s_b, int32_t* s_n, uint64_t* s_fin,
-                                           int32_t ln0, int64_t b0, bool probe, uint64_t ffm = 0ull,
-                                           uint64_t U0 = 0ull)
+                                           int32_t ln0, int64_t b0, bool probe)
 {
     const int lane = lane_id();
     {
         const size_t li = (size_t)t * TILE + lane;
         const bool o = (occ >> lane) & 1ull;
-        int32_t ln = o ? ln0 : 0;
-        bool unsat = (U >> lane) & 1ull;
-        if ((ffm >> lane) & 1ull) {
-            if ((U0 >> lane) & 1ull) ln = 1;        // iteration 0 unsatisfied: iteration 1 decides
-            else { ln = 0; unsat = false; }         // Init's decisions are a codeword: iters 0
-        }
+        const int32_t ln = o ? ln0 : 0;
+        const bool unsat = (U >> lane) & 1ull;
         const bool fin = o && (!unsat || ln == max_iter);
         const bool cont = o && !fin;
         const int64_t b = o ? b0 : -1;
@@ -216,17 +202,16 @@ __device__ __forceinline__ uint64_t row_parity(const uint64_t* __restrict__ h, c
 // lane bookkeeping for the step (cont_lanes: iters / valid, refill claims,
 // active / fresh / occupied masks) and hands the finished lanes to the
 // variable kernel, which writes their outputs before refilling them.
-// p0: the block's OR of iteration-0 row parities (FirstCheck, rs.unsat0 set).
 __device__ __forceinline__ void res_arrive(int64_t t, uint64_t occ, uint64_t p, const ResStep& rs, int32_t ln0,
-                                           int64_t b0, uint32_t nblk, uint64_t p0 = 0ull)
+                                           int64_t b0, uint32_t nblk)
 {
-    __shared__ uint64_t red[4], red0[4];
+    __shared__ uint64_t red[4];
     __shared__ int64_t s_b[TILE];
     __shared__ int32_t s_n[TILE];
     __shared__ uint64_t s_fin;
     __shared__ int s_last;
     const int lane = lane_id(), w = wave_id();
-    if (lane == 0) { red[w] = p; red0[w] = p0; }
+    if (lane == 0) red[w] = p;
     __syncthreads();
     // No fences: an agent-scope release would write back the L2 in every
     // block.  Only device-coherent atomics carry data between the blocks; the
@@ -235,29 +220,22 @@ __device__ __forceinline__ void res_arrive(int64_t t, uint64_t occ, uint64_t p, 
     // bookkeeping reads was written by earlier kernels.
     if (threadIdx.x == 0) {
         const uint64_t U = red[0] | red[1] | red[2] | red[3];
-        const uint64_t U0 = red0[0] | red0[1] | red0[2] | red0[3];
-        unsigned long long o = 0, o0 = 0;
+        unsigned long long o = 0;
         if (U) o = atomicOr(rs.unsat + t, (unsigned long long)U);
-        if (U0) o0 = atomicOr(rs.unsat0 + t, (unsigned long long)U0);
-        asm volatile("" ::"v"(o), "v"(o0) : "memory");
+        asm volatile("" ::"v"(o) : "memory");
         s_last = atomicAdd(rs.done + t, 1u) == nblk - 1;
     }
     __syncthreads();
     if (!s_last) return;
     if (threadIdx.x < TILE) {
         const uint64_t U = occ ? (uint64_t)atomicOr(rs.unsat + t, 0ull) : 0ull;
-        // lanes refilled at the previous step with their first check from codes
-        // (read before cont_lanes rewrites the fresh mask)
-        const uint64_t ffm = rs.unsat0 ? (rs.cs.fresh[t] & occ) : 0ull;
-        const uint64_t U0 = ffm ? (uint64_t)atomicOr(rs.unsat0 + t, 0ull) : 0ull;
-        cont_lanes(t, occ, U, rs.max_iter, rs.cs, rs.co, s_b, s_n, &s_fin, ln0, b0, false, ffm, U0);
+        cont_lanes(t, occ, U, rs.max_iter, rs.cs, rs.co, s_b, s_n, &s_fin, ln0, b0, false);
         const size_t li = (size_t)t * TILE + lane;
         rs.fin_b[li] = s_b[lane];
         rs.fin_n[li] = s_n[lane];
         if (lane == 0) {
             rs.fin[t] = s_fin;
             atomicExch(rs.unsat + t, 0ull);
-            if (rs.unsat0) atomicExch(rs.unsat0 + t, 0ull);
             atomicExch(rs.done + t, 0u);
         }
     }
@@ -1071,83 +1049,6 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
                    (i1 < 0 ? MSA_META_NONE : ((uint32_t)(row * DC + i1) & MSA_META_ID)));
 }
 
-// First check from codes (FirstCheck), after k_check_msa_c on the same
-// group: the records of the lanes claimed at this step's syndrome, from their
-// input codes -- Init_MSA_INF (dec.cpp:1300-1329) sets every v2c of column j
-// to LLR_j, so row r's inputs are its columns' LLRs -- with k_check_msa_c's
-// arithmetic (one pass: min1 with its first index, min2 over the others, the
-// sign parity of !(x >= 0), the NaN planes of x_0 / x_1), and the parity of
-// Init's decisions !(LLR > 0) over the row (the iteration-0 syndrome,
-// dec.cpp:1223) into fc.u0_rows.  Only the refilled lanes run (k_check_msa_c
-// skips lines with no live lane and writes garbage records for refilled lanes
-// in lines with one); a separate launch keeps the byte gathers and table
-// lookups off the streaming kernel's critical path.  grid (ceil(M/4), group
-// tiles), block 256; the table in LDS.
-template <int DC>
-__global__ __launch_bounds__(256) void k_check_msa_c_first(double* __restrict__ rec, uint16_t* __restrict__ meta,
-                                                           int32_t M, int64_t t0, FirstCheck fc)
-{
-    __shared__ double tab[256];
-    const int64_t t = t0 + blockIdx.y;
-    const uint64_t frm = fc.fresh[t];
-    if (frm == 0ull) return;  // block-uniform
-    tab[threadIdx.x] = fc.ptab[threadIdx.x];
-    __syncthreads();
-    const int lane = lane_id();
-    const int32_t row = blockIdx.x * 4 + wave_id();
-    if (row >= M) return;
-    const bool fr = (frm >> lane) & 1ull;
-    uint32_t p0 = 0;
-    if (fr) {
-        // a tile's refills hold consecutive codewords (one claim per tile,
-        // cont_lanes): one buffer resource over their input rows
-        const int64_t bmin = fc.lane_b[t * TILE + __builtin_ctzll(frm)];
-        const int64_t bl = fc.lane_b[t * TILE + lane];
-        const auto rin = buf_rsrc(fc.in_code + (size_t)bmin * fc.N, (uint64_t)TILE * fc.N);
-        const int voff = (int)(bl - bmin) * fc.N;
-        const int32_t* __restrict__ cols = fc.col_idx + (size_t)row * DC;  // wave-uniform: scalar loads
-        double m1 = __builtin_inf(), m2 = __builtin_inf(), a0 = 0.0, a1 = 0.0;
-        int i1 = -1;
-        uint32_t neg = 0;
-        // chunks of CH gathers in flight (all DC at once would hold DC
-        // registers and halve the occupancy that hides their latency)
-        constexpr int CH = 24;
-#pragma unroll 1
-        for (int k0 = 0; k0 < DC; k0 += CH) {
-            int32_t k8[CH];
-#pragma unroll
-            for (int i = 0; i < CH; ++i)
-                if (k0 + i < DC) k8[i] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rin, voff, cols[k0 + i], 0);
-#pragma unroll
-            for (int i = 0; i < CH; ++i) {
-                const int k = k0 + i;
-                if (k >= DC) break;
-                const double x = tab[k8[i] + kCodeBias];
-                const double a = __builtin_fabs(x);
-                if (k == 0) a0 = a;
-                if (k == 1) a1 = a;
-                neg ^= (x >= 0) ? 0u : 1u;
-                p0 ^= (x > 0) ? 0u : 1u;  // Init_MSA_INF's decision !(LLR > 0)
-                const bool lt1 = a < m1, lt2 = a < m2;
-                m2 = lt1 ? m1 : (lt2 ? a : m2);
-                m1 = lt1 ? a : m1;
-                i1 = lt1 ? k : i1;
-            }
-        }
-        const bool nan0 = __builtin_isnan(a0), nan1 = __builtin_isnan(a1);
-        double* __restrict__ r = rec + ((size_t)blockIdx.y * M + row) * (MSA_REC_PLANES * TILE) + lane;
-        r[0] = m1;
-        r[TILE] = m2;
-        if (nan0) r[2 * TILE] = a0;
-        if (nan1) r[3 * TILE] = a1;
-        meta[((size_t)blockIdx.y * M + row) * TILE + lane] =
-            (uint16_t)((neg << 15) | ((nan1 ? 1u : 0u) << 14) | ((nan0 ? 1u : 0u) << 13) |
-                       (i1 < 0 ? MSA_META_NONE : ((uint32_t)(row * DC + i1) & MSA_META_ID)));
-    }
-    const uint64_t pm = __ballot(fr && p0 != 0u);
-    if (lane == 0) fc.u0_rows[(size_t)t * M + row] = pm;
-}
-
 __device__ __forceinline__ double flip_sign(double v, uint32_t neg)
 {
     return __longlong_as_double(__double_as_longlong(v) ^ ((long long)(neg & 1u) << 63));
@@ -1174,11 +1075,8 @@ __device__ __forceinline__ uint32_t er_pos(uint32_t er, int DC)
 // record loads (their plane depends on the meta word), all through buffer
 // resources (per-edge offsets in SGPRs); NT: nontemporal v2c stores (the
 // group's v2c is read back once, by the next check phase).  PC: coded
-// priors, as k_var_m.  FF (FirstCheck, with CONT and PC): a refilled lane's
-// first check ran in this step's check kernel, so it runs its first update
-// here (prior = its codes' LLR, own v2c signs = the LLR's sign, as Init_MSA_INF
-// left them) instead of Init_MSA_INF's stores.
-template <int DC, int DV, bool CONT, int CPW, bool NT, bool PC = false, bool FF = false>
+// priors, as k_var_m.
+template <int DC, int DV, bool CONT, int CPW, bool NT, bool PC = false>
 __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ rec, const uint16_t* __restrict__ meta,
                                                    double* __restrict__ v2c,
                                                    double* __restrict__ prior, uint64_t* __restrict__ hard,
@@ -1216,7 +1114,6 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
     const auto rmeta = buf_rsrc(meta + (size_t)ty * M * TILE, (uint64_t)M * TILE * sizeof(uint16_t));
     const auto rv2c = buf_rsrc(v2c + (size_t)t * E * TILE, (uint64_t)E * TILE * sizeof(double));
     static_assert(CONT || !PC, "coded priors come with continuous refills");
-    static_assert(!FF || (CONT && PC), "first check from codes: coded continuous refills");
     double l[CPW][DV], pv[CPW], xin[CPW];
     int8_t kin[CPW];  // PC: the refilled lane's input codes
     if (fr) {
@@ -1227,10 +1124,8 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             else xin[c] = rf.in[rb + j0 + c];
         }
     }
-    // lanes updated this step: the live ones, and with FF the refilled ones
-    const bool upd = live || (FF && fr);
     uint32_t cpk[CPW];  // per edge: c2v sign (bit 0) and record plane (bits 1-2), 4 bits each
-    if (upd) {
+    if (live) {
         // the meta words first; from them, per edge a 4-bit code (bit 0: the
         // c2v sign = parity ^ own sign, bits 1-2: the record plane -- m2 at the
         // row's min1 edge, a NaN plane when x_0 / x_1 is NaN, else m1), packed
@@ -1241,13 +1136,8 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
         uint32_t sb[CPW], mw[CPW][DV];  // mw: the u16 meta words
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
-            if (FF && fr) {  // Init_MSA_INF's state: prior LLR, every own v2c = LLR
-                pv[c] = rf.ptab[kin[c] + kCodeBias];
-                sb[c] = (pv[c] >= 0) ? 0u : 0xffu;
-            } else {
-                pv[c] = prior_at<PC>(prior, rf, ((size_t)t * N + j0 + c) * TILE + lane);
-                sb[c] = sgn[((size_t)t * N + j0 + c) * TILE + lane];
-            }
+            pv[c] = prior_at<PC>(prior, rf, ((size_t)t * N + j0 + c) * TILE + lane);
+            sb[c] = sgn[((size_t)t * N + j0 + c) * TILE + lane];
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
                 const int rid = (int)(er[c][s] >> MSA_ER_SHIFT);
@@ -1290,31 +1180,23 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
     }
     // a refill's prior value: its table lookup goes out behind the record
     // loads (waiting only for its code), so the two latencies overlap
-    if constexpr (PC && !FF) {
+    if constexpr (PC) {
         if (fr) {
 #pragma unroll
             for (int c = 0; c < CPW; ++c) xin[c] = rf.ptab[kin[c] + kCodeBias];
         }
     }
-    if (upd) {
+    if (live) {
 #pragma unroll
         for (int c = 0; c < CPW; ++c)
 #pragma unroll
             for (int s = 0; s < DV; ++s) l[c][s] = flip_sign(l[c][s], cpk[c] >> (4 * s));
     }
-    if (CONT && fl) {
-        // finished codeword: hard bits of its exit -- the ballots before this
-        // step's update, or at iteration 0 Init_MSA_INF's decisions !(LLR > 0)
-        // (with FF the ballots already hold its first update's)
-        uint64_t v = 0;
+    if (CONT && fl) {  // finished codeword: hard bits of its exit (ballots before this step's update)
+        uint64_t hw[CPW];
 #pragma unroll
-        for (int c = 0; c < CPW; ++c) {
-            const size_t pj = ((size_t)t * N + j0 + c) * TILE + lane;
-            const bool hb = fn > 0 ? ((hard[(size_t)t * N + j0 + c] >> lane) & 1ull) != 0ull
-                                   : !(prior_at<PC>(prior, rf, pj) > 0);
-            v |= (uint64_t)hb << (8 * c);
-        }
-        store_fin_bytes<CPW>(rf, v, fb, N, j0);
+        for (int c = 0; c < CPW; ++c) hw[c] = hard[(size_t)t * N + j0 + c];
+        store_fin_hard<CPW>(rf, hw, fb, N, j0, lane);
     }
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
@@ -1328,12 +1210,12 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
         double dv[DV];
 #pragma unroll
         for (int s = 0; s < DV; ++s) dv[s] = 0.0;
-        if (!FF && fr) {  // Init_MSA_INF for a refilled lane
+        if (fr) {  // Init_MSA_INF for a refilled lane
             const double x = xin[c];
 #pragma unroll
             for (int s = 0; s < DV; ++s) dv[s] = x;
             h = !(x > 0);
-        } else if (upd) {
+        } else if (live) {
             // v2c_s = LLR + c_0 + ... (skipping c_s), L = LLR + all, in the
             // reference's left-to-right order: v2c_s continues the shared
             // prefix P_s = LLR + c_0 + ... + c_{s-1} with c_{s+1} .. c_{DV-1}
@@ -1354,7 +1236,6 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             else prior[pj] = xin[c];
         }
         if (line_occupied(touched, lane) || fr || live) {  // whole-line stores, as k_var_m
-            // (a refilled lane's v2c: Init's copies of its LLR, or with FF its first update's)
             uint32_t sbn = 0;
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
@@ -1424,7 +1305,6 @@ __global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ pos
 __global__ __launch_bounds__(256) void k_cont_reset(uint64_t* __restrict__ active, uint64_t* __restrict__ fresh,
                                                     uint64_t* __restrict__ occupied, unsigned long long* __restrict__ ctr,
                                                     int32_t nctr, unsigned long long* __restrict__ unsat,
-                                                    unsigned long long* __restrict__ unsat0,
                                                     unsigned* __restrict__ done, int64_t tiles)
 {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tiles; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1432,7 +1312,6 @@ __global__ __launch_bounds__(256) void k_cont_reset(uint64_t* __restrict__ activ
         fresh[i] = 0;
         occupied[i] = 0;
         if (unsat) unsat[i] = 0;
-        if (unsat0) unsat0[i] = 0;
         if (done) done[i] = 0;
     }
     if (blockIdx.x == 0 && (int32_t)threadIdx.x < nctr) ctr[threadIdx.x] = 0;
@@ -1455,10 +1334,7 @@ __global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs)
     const int lane = lane_id();
     int32_t ln0 = 0;
     int64_t b0 = 0;
-    uint64_t u = 0, u0 = 0;
-    // FirstCheck: lanes refilled at the previous step; their iteration-0 row
-    // parities are in u0_rows (written by that step's check kernel)
-    const bool ff = rs.u0_rows && occ && (rs.cs.fresh[t] & occ);
+    uint64_t u = 0;
     if (occ) {
         if (threadIdx.x < TILE && ((occ >> lane) & 1ull)) {
             ln0 = rs.cs.lane_n[t * TILE + lane];
@@ -1477,7 +1353,6 @@ __global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs)
                     if (k < DC) p ^= h[cols[k]];
                 }
             }
-            if (ff && part == 0 && row < M) u0 |= rs.u0_rows[(size_t)t * M + row];
             p ^= shfl_xor_u64(p, 8);
             p ^= shfl_xor_u64(p, 16);
             p ^= shfl_xor_u64(p, 32);
@@ -1486,12 +1361,8 @@ __global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs)
         u |= shfl_xor_u64(u, 1);
         u |= shfl_xor_u64(u, 2);
         u |= shfl_xor_u64(u, 4);
-        if (ff) {
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) u0 |= shfl_xor_u64(u0, off);
-        }
     }
-    res_arrive(t, occ, u, rs, ln0, b0, gridDim.x, u0);
+    res_arrive(t, occ, u, rs, ln0, b0, gridDim.x);
 }
 
 // hard ballots -> [b][N] u8 (the reference's dblk / dec_*.txt bits)

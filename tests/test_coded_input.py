@@ -205,15 +205,12 @@ def test_host_api_negative_zero_and_off_lattice(G, og, codewords, algo):
 
 @pytest.mark.timeout(180)
 @pytest.mark.parametrize("max_iter", [1, 2, 50])
-def test_msa_first_check_from_codes(gpu, G, og, codewords, max_iter):
-    """Compressed min-sum on coded input runs every refill's first check from
-    its codes in the step that claims it (dev::FirstCheck), evaluating
-    iterations 0 and 1 together at the next syndrome.  Over several pool fills
-    (2500 codewords through the 1024-lane pool, so refills land in tiles with
-    live lanes), with noiseless rows (iteration-0 exits: outputs from Init's
-    decisions) and max_iter 1 / 2 / 50: identical hard bits, posterior,
-    iterations and valid flags to the same engine kind with an Init step
-    (first_from_prior off), and a sample equal to the oracle."""
+def test_msa_coded_refills_over_several_fills(gpu, G, og, codewords, max_iter):
+    """The compressed min-sum's coded refills over several pool fills (2500
+    codewords through the 1024-lane pool, so refills land in tiles with live
+    lanes), with noiseless rows (iteration-0 exits) and max_iter 1 / 2 / 50:
+    identical hard bits, posterior, iterations and valid flags to the fp64
+    input, and a sample from both ends and the middle equal to the oracle."""
     L = gpu
     N, B = G.N, 2500
     llr = synth.bsc_llrs(codewords, 0, B, seed=77, p=0.002)
@@ -221,23 +218,23 @@ def test_msa_first_check_from_codes(gpu, G, og, codewords, max_iter):
     k = np.rint(llr / synth.LLR_UNIT).astype(np.int8)
     codes = L.DeviceBuffer(0, B * N)
     codes.upload(k)
-    outs = []
-    for ffp in (True, False):
-        eng = L.Engine(G, 0, "msa", first_from_prior=ffp)
-        assert eng.msa_compressed and eng.continuous and eng.first_from_prior == ffp
-        outs.append(_run(L, eng, B, N, lambda h, pp, it, v: eng.decode_codes(
-            codes.at(0), _table(), L.IN_LLR, B, max_iter, h, pp, L.POST_LLR, it, v)))
-        eng.close()
-    _same(outs[0], outs[1])
-    it = outs[0][2]
-    assert (it[::7] == 0).all() and outs[0][3][::7].all()
+    fp = L.DeviceBuffer(0, B * N * 8)
+    fp.upload(llr)
+    eng = L.Engine(G, 0, "msa")
+    assert eng.msa_compressed and eng.continuous and eng.cap < B
+    a = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode_codes(codes.at(0), _table(), L.IN_LLR, B, max_iter, h, pp,
+                                                                 L.POST_LLR, it, v))
+    b = _run(L, eng, B, N, lambda h, pp, it, v: eng.decode(fp.at(0), L.IN_LLR, B, max_iter, h, pp, L.POST_LLR, it, v))
+    _same(a, b)
+    it = a[2]
+    assert (it[::7] == 0).all() and a[3][::7].all()
     if max_iter == 50:
         assert len(np.unique(it)) > 5
     idx = np.unique(np.concatenate([np.arange(0, 21), np.arange(B - 20, B), np.arange(1000, 1030)]))
     rh, rp, rit, rv = og.decode_batch(llr[idx], max_iter, algo=1, post_mode=0, threads=8)
-    a = outs[0]
     assert np.array_equal(a[0][idx], rh) and np.array_equal(a[2][idx], rit) and np.array_equal(a[3][idx], rv)
     assert np.array_equal(a[1][idx].view(np.uint64), rp.view(np.uint64))
+    eng.close()
 
 
 @pytest.mark.parametrize("algo,kw", [("bp", {}), ("bp", dict(chunk=64, devices=[0, 0])), ("msa", {}),
