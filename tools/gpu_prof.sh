@@ -21,7 +21,7 @@ if [ "$WHICH" = msa ] || [ "$WHICH" = both ]; then
   run trace_msa 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_msa" -o run --output-format csv -- python3 "$R/bench.py" \
     --algo msa --p 0.002 --batch-per-gpu 1000000 --steps 1 --warmup 1 --cpu-baseline 0 --secondary 0
   rm -f "$OUT"/trace_msa/*kernel_trace.csv
-  B="python3 $R/bench.py --algo msa --p 0.002 --cpu-baseline 0 --secondary 0 --no-profile --steps 1 --warmup 0 --batch-per-gpu 16384"
+  B="python3 $R/bench.py --algo msa --p 0.002 --cpu-baseline 0 --secondary 0 --no-profile --steps 1 --warmup 0 --batch-per-gpu ${MSA_B:-16384}"
   for grp in "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
              "TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum" \
              "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"; do
@@ -33,7 +33,7 @@ if [ "$WHICH" = bp ] || [ "$WHICH" = both ]; then
   run trace_bp 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_bp" -o run --output-format csv -- python3 "$R/bench.py" \
     --cpu-baseline 0 --secondary 0
   rm -f "$OUT"/trace_bp/*kernel_trace.csv
-  B="python3 $R/bench.py --cpu-baseline 0 --secondary 0 --no-profile --steps 1 --warmup 0 --batch-per-gpu 8192"
+  B="python3 $R/bench.py --cpu-baseline 0 --secondary 0 --no-profile --steps 1 --warmup 0 --batch-per-gpu ${BP_B:-8192}"
   for grp in "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "FETCH_SIZE" "WRITE_SIZE"; do
     tagg=$(echo "$grp" | tr ' ' '+')
     run "bp_$tagg" 120 rocprofv3 --pmc $grp -d "$OUT/bp/pmc_$tagg" -o run --output-format csv -- $B
