@@ -39,7 +39,7 @@
 
 namespace ldpc {
 
-// Defaults, each chosen by a same-process A/B on MI355X.
+// Defaults, each chosen by a same-process A/B on MI355X (profiles/r*/README.md).
 constexpr int32_t kDefaultGroupTiles = 3;     // grouped schedule (tools/sweep.py)
 constexpr int32_t kDefaultMsaGroupTiles = 4;  // compressed min-sum, 1024-lane pool
 constexpr int32_t kDefaultVarCpw = 4;         // fp64 priors: +2.6-2.9 % over 1 column per wave
