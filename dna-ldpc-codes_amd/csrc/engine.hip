@@ -953,6 +953,13 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         LAUNCH(K_SYN, klaunch(k_syndrome_split<72>, dim3((unsigned)syn_blocks, (unsigned)tiles), dim3(256), 0,
                               stream, M, rs));
         const int64_t gstep = low ? std::max(group_tiles, c2v_tiles) : group_tiles;
+        if (ffp && cur_codes && s == 0 && N % 64 == 0) {
+            // single fill on codes: step 0 is the transpose of the claimed
+            // rows into the lane codes (+ Init's decision ballots)
+            LAUNCH(K_INIT, klaunch(k_fill_codes, dim3((unsigned)(N / 64), (unsigned)tiles), dim3(256), 0, stream,
+                                   cur_codes, d_lane_b, d_fresh, pcode, d_ptab, hard, N));
+            continue;  // (the poll of step 0 is never awaited: lag 1 waits from step 1 on)
+        }
         for (int64_t t0 = 0; t0 < tiles; t0 += gstep) {
             const unsigned gt = (unsigned)std::min<int64_t>(gstep, tiles - t0);
             int rc;

@@ -506,6 +506,45 @@ __global__ __launch_bounds__(256, 2) void k_check_bp_first(const double* __restr
     check_bp_compute<DC, false>(x, lr + ((size_t)blockIdx.y * E + (size_t)row * DC) * TILE + lane);
 }
 
+// Step 0 of a single-fill coded BP decode (the DNA batch): every occupied
+// lane was just refilled (Refill::prior_only), so the refill is a transpose
+// of the claimed codewords' input rows ([b][N] int8) into the tiles' lane
+// codes ([t][N][64], Refill::pcode) plus the ballots of Init_Belief_
+// Propagation's decisions LR < 1 (dec.cpp:608-629; LR = ptab[code + 128]).
+// Through LDS, 64 columns x 64 lanes per block: each input row segment is
+// read as 64 contiguous bytes and each lane-code segment written as 64 --
+// instead of the variable kernel's per-lane byte gathers.  N % 64 == 0;
+// grid (N / 64, tiles), block 256.
+__global__ __launch_bounds__(256) void k_fill_codes(const int8_t* __restrict__ in_code,
+                                                    const int64_t* __restrict__ lane_b,
+                                                    const uint64_t* __restrict__ fresh, int8_t* __restrict__ pcode,
+                                                    const double* __restrict__ ptab, uint64_t* __restrict__ hard,
+                                                    int32_t N)
+{
+    __shared__ int8_t sc[TILE][TILE + 4];
+    __shared__ int64_t sb[TILE];
+    const int64_t t = blockIdx.y;
+    const uint64_t frm = fresh[t];
+    if (frm == 0ull) return;  // block-uniform
+    const int lane = lane_id(), w = wave_id();
+    const int32_t j0 = (int32_t)blockIdx.x * TILE;
+    if (threadIdx.x < TILE) sb[lane] = ((frm >> lane) & 1ull) ? lane_b[t * TILE + lane] : -1;
+    __syncthreads();
+    for (int l = w; l < TILE; l += 4) {
+        const int64_t b = sb[l];
+        sc[l][lane] = b >= 0 ? in_code[(size_t)b * N + j0 + lane] : (int8_t)0;
+    }
+    __syncthreads();
+    const bool fr = (frm >> lane) & 1ull;
+    for (int c = w; c < TILE; c += 4) {
+        const int8_t k = sc[lane][c];
+        const size_t o = (size_t)t * N + j0 + c;
+        pcode[o * TILE + lane] = k;
+        const uint64_t m = __ballot(fr && ptab[k + kCodeBias] < 1.0);
+        if (lane == 0) hard[o] = (frm == ~0ull) ? m : ((hard[o] & ~frm) | m);
+    }
+}
+
 // grid (ceil(M/4), tiles t0 .. t0+gridDim.y-1); lr: the group's c2v scratch
 // ([t - t0][E][64]), or with RES the pool's messages themselves (in place).
 template <int DC, bool NT, bool RES>
