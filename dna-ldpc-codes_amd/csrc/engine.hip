@@ -883,9 +883,11 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         rf.ptab = d_ptab;
     }
     // A batch that fits the lane pool in one fill (the DNA batch) polls one
-    // step behind instead of kLag: its steps take >= 30 us, time enough to
-    // enqueue the next, and the decode ends one empty step sooner.
-    const int lag = B <= tiles * 64 ? 1 : kLag;
+    // step behind instead of kLag in the resident pool, and in the grouped
+    // schedule waits for the step's own poll (below): its steps take >= 30
+    // us, time enough to enqueue the next, and the decode ends sooner.
+    const bool single_fill = B <= tiles * 64;
+    const int lag = single_fill ? 1 : kLag;
     // Host step bound.  A lane finishes its codeword at most max_iter + 2
     // steps after claiming it (refill step, max_iter iterations, the final
     // syndrome), so within every window of max_iter + 2 steps each lane either
@@ -942,7 +944,12 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
     // device by kLag.
     bool low = false;
     // single fill: step 0's refill stores only the prior, step 1's check reads it
-    const bool ffp = first_fp && B <= tiles * 64 && c2v != v2c;
+    const bool ffp = first_fp && single_fill && c2v != v2c;
+    // single fill: wait for the step's own poll -- its syndrome (and with it
+    // the poll word) comes first, so the answer arrives while the step's
+    // check / variable launches still run, and no empty step follows the
+    // drain; step 0 (claims and refills only) is not awaited
+    const int glag = single_fill ? 0 : lag;
     Refill rf0 = rf;
     rf0.prior_only = ffp ? 1 : 0;
     const int64_t limit = step_limit(1);
@@ -958,7 +965,7 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             // rows into the lane codes (+ Init's decision ballots)
             LAUNCH(K_INIT, klaunch(k_fill_codes, dim3((unsigned)(N / 64), (unsigned)tiles), dim3(256), 0, stream,
                                    cur_codes, d_lane_b, d_fresh, pcode, d_ptab, hard, N));
-            continue;  // (the poll of step 0 is never awaited: lag 1 waits from step 1 on)
+            continue;  // (the poll of step 0 is never awaited)
         }
         for (int64_t t0 = 0; t0 < tiles; t0 += gstep) {
             const unsigned gt = (unsigned)std::min<int64_t>(gstep, tiles - t0);
@@ -978,9 +985,9 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
             }
             if ((rc = launch_var(stream, c2v, t0, gt, pt, s == 0 ? rf0 : rf))) return rc;
         }
-        if (q >= q0 + (uint64_t)lag) {
+        if (q >= q0 + (uint64_t)glag && s > 0) {
             unsigned long long occ = 0;
-            if (int r = poll_wait(q - lag, &occ)) return r;
+            if (int r = poll_wait(q - glag, &occ)) return r;
             if (drained(occ)) break;
             low = occ * 32 < (unsigned long long)(tiles * 64);
         }
