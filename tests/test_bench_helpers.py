@@ -1,0 +1,58 @@
+"""bench.py's host-side helpers on CPU (no GPU): the oracle-check row
+selection and the roofline block's algorithmic / moved byte accounting."""
+import importlib.util
+import os
+import types
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_tail_and_interior_rows():
+    b = _bench()
+    for B, lo in ((100_000, 200), (1_000_000, 32), (129, 16), (40, 30), (10, 10)):
+        tail, inter = b.tail_and_interior(B, lo, seed=7)
+        rows = np.concatenate([np.arange(lo), tail, inter])
+        assert len(np.unique(rows)) == len(rows)  # disjoint
+        assert rows.max() < B and (tail.size == 0 or tail[-1] == B - 1)
+        assert np.all(np.diff(inter) > 0) and (inter.size == 0 or (inter.min() >= lo and inter.max() < B - 32))
+        assert inter.size == min(32, max(0, B - 32 - lo))
+
+
+def _eng(**kw):
+    d = dict(msa_compressed=False, resident=True, continuous=True, nontemporal=False, algo=0)
+    d.update(kw)
+    return types.SimpleNamespace(**d)
+
+
+def test_roofline_moved_bytes():
+    b = _bench()
+    G = types.SimpleNamespace(N=18432, M=2048, E=147456)
+    st = {"check": {"ms": 0.07, "sampled": 1, "launches": 100}, "variable": {"ms": 0.068, "sampled": 1, "launches": 100},
+          "syndrome": {"ms": 0.0, "sampled": 0, "launches": 0}}
+    cw_iters = 100 * 192.0
+    r = b.roofline(_eng(), G, st, cw_iters, coded=True)
+    assert r["kernel"].startswith("k_check_bp")  # dominant
+    assert r["achieved_moved"] == r["achieved"]  # the check kernel reads no prior
+    assert r["iteration_bytes_per_cw_iter"]["survey_8d"] == 32 * G.E + 10 * G.N
+    assert r["iteration_bytes_per_cw_iter"]["moved"] == 16 * G.E + 16 * G.E + 8 * G.N + G.N / 8 - 7 * G.N
+    assert r["iteration_GBps_moved"] < r["iteration_GBps"]
+    # compressed min-sum: the variable kernel dominates; moved = algorithmic - 7 N with coded priors
+    st["variable"]["ms"] = 0.0713
+    st["check"]["ms"] = 0.049
+    rm = b.roofline(_eng(msa_compressed=True, resident=False, nontemporal=True, algo=1), G, st, cw_iters, coded=True)
+    assert rm["kernel"].startswith("k_var_msa_c")
+    assert rm["moved_bytes_per_cw_iter"] == rm["algorithmic_bytes_per_cw_iter"] - 7 * G.N
+    assert abs(rm["achieved_moved"] / rm["achieved"] - rm["moved_bytes_per_cw_iter"] /
+               rm["algorithmic_bytes_per_cw_iter"]) < 1e-3
+    assert rm["frac_of_measured_ceiling"] == round(rm["achieved_moved"] / rm["ceiling_measured"], 4)
+    rf = b.roofline(_eng(msa_compressed=True, resident=False, nontemporal=True, algo=1), G, st, cw_iters, coded=False)
+    assert rf["achieved_moved"] == rf["achieved"]
