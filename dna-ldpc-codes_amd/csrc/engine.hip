@@ -122,7 +122,7 @@ Engine::~Engine()
     for (auto e : ev_pool) hipEventDestroy(e);
     hipFree(d_fresh); hipFree(d_occ); hipFree(d_lane_b); hipFree(d_lane_n); hipFree(d_ctr);
     if (h_poll) hipHostFree(h_poll);
-    hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge); hipFree(d_col_er);
+    hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge); hipFree(d_col_er); hipFree(d_row_pos);
     hipFree(d_unsat); hipFree(d_done); hipFree(d_fin); hipFree(d_fin_b); hipFree(d_fin_n);
     hipFree(d_sgn);
     hipFree(v2c); if (c2v != v2c) hipFree(c2v); hipFree(prior); hipFree(hard); hipFree(active); hipFree(iters); hipFree(valid);
@@ -224,6 +224,11 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         for (size_t q = 0; q < er.size(); q++)
             er[q] = ((uint32_t)g->edge_row[(size_t)g->col_edge[q]] << dev::MSA_ER_SHIFT) | (uint32_t)g->col_edge[q];
         if ((rc = upload(&d_col_er, er))) return rc;
+        // CSR edge -> its CSC position: the compressed min-sum keeps v2c in
+        // column order (contiguous variable-phase stores, gathered check reads)
+        std::vector<int32_t> pos(g->col_edge.size());
+        for (size_t q = 0; q < pos.size(); q++) pos[(size_t)g->col_edge[q]] = (int32_t)q;
+        if ((rc = upload(&d_row_pos, pos))) return rc;
     }
     if (g->regular_dc && g->dc_max > 0) {
         std::vector<int32_t> T((size_t)g->dc_max * g->M);
@@ -448,10 +453,10 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
     if (msa_c) {
         if (nt_d)
             LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, true>), grid, blk, 0, s, v2c, msa_rec(scratch),
-                                          msa_meta(scratch, c2v_tiles, M), active, M, E, t0));
+                                          msa_meta(scratch, c2v_tiles, M), active, d_row_pos, M, E, t0));
         else
             LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, false>), grid, blk, 0, s, v2c, msa_rec(scratch),
-                                          msa_meta(scratch, c2v_tiles, M), active, M, E, t0));
+                                          msa_meta(scratch, c2v_tiles, M), active, d_row_pos, M, E, t0));
         return LDPC_OK;
     }
     if (reg72) {

@@ -288,7 +288,8 @@ __global__ __launch_bounds__(256) void k_init(const double* __restrict__ in, int
         }
         prior[((size_t)t * N + j) * TILE + lane] = pv;
         const int32_t a = col_ptr[j], e1 = col_ptr[j + 1];
-        for (int32_t q = a; q < e1; ++q) v2c[((size_t)t * E + col_edge[q]) * TILE + lane] = m;
+        // (the compressed min-sum -- sgn set -- keeps v2c in column order)
+        for (int32_t q = a; q < e1; ++q) v2c[((size_t)t * E + (sgn ? q : col_edge[q])) * TILE + lane] = m;
         // compressed min-sum without codes: sign bits of the stored v2c (all edges alike)
         if (sgn) sgn[((size_t)t * N + j) * TILE + lane] = (m >= 0) ? 0u : 0xffu;
         const uint64_t hm = __ballot(h && inb);
@@ -1039,7 +1040,8 @@ constexpr uint32_t MSA_META_NONE = 0x1000u;  // meta bit 12: no min1 (never equa
 template <int DC, bool NT>
 __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, double* __restrict__ rec,
                                                      uint16_t* __restrict__ meta, const uint64_t* __restrict__ active,
-                                                     int32_t M, int64_t E, int64_t t0)
+                                                     const int32_t* __restrict__ row_pos, int32_t M, int64_t E,
+                                                     int64_t t0)
 {
     static_assert(DC >= 2 && DC <= 96, "row degree");
     const int lane = lane_id();
@@ -1050,11 +1052,14 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     if (!(row < M && line_occupied(act, lane))) return;
     // the row's DC segments through a buffer resource: per-edge offsets in
     // the instructions, one per-lane VGPR offset (no 64-bit addresses)
-    const auto rv2c = buf_rsrc(v2c + ((size_t)t * E + (size_t)row * DC) * TILE, (uint64_t)DC * TILE * 8);
+    // v2c is in column (CSC) order: the row's DC segments are gathered
+    // through the CSR -> CSC position table (wave-uniform: scalar loads)
+    const auto rv2c = buf_rsrc(v2c + (size_t)t * E * TILE, (uint64_t)E * TILE * 8);
+    const int32_t* __restrict__ pos = row_pos + (size_t)row * DC;
     double x[DC];
 #pragma unroll
     for (int k = 0; k < DC; ++k)
-        x[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv2c, lane * 8, k * (TILE * 8),
+        x[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv2c, lane * 8, pos[k] * (TILE * 8),
                                                                                NT ? kBufNT : 0));
     // one pass: min1 with its FIRST index, min2 = minimum over the other
     // indices (a tie with min1 gives min2 == min1), NaN never compares less
@@ -1278,9 +1283,9 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             uint32_t sbn = 0;
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
-                const int eid = (int)(er[c][s] & MSA_ER_EDGE);
+                // v2c in column order: the wave's CPW x DV stores are one contiguous run
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, dv[s]), rv2c, lane * 8,
-                                                      eid * (TILE * 8), NT ? kBufNT : 0);
+                                                      ((j0 + c) * DV + s) * (TILE * 8), NT ? kBufNT : 0);
                 sbn |= (dv[s] >= 0 ? 0u : 1u) << s;
             }
             sgn[pj] = (uint8_t)sbn;
