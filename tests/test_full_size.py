@@ -119,7 +119,7 @@ def test_config5_exact_workload(gpu, G, og, codewords):
     v = dv.download(np.empty(B, np.uint8)).astype(bool)
     assert (it >= 0).all() and (it <= max_iter).all()
     assert (it[~v] == max_iter).all(), "an invalid codeword stopped early"
-    assert 0.99 < v.mean() < 1.0, v.mean()
+    assert 0.93 < v.mean() < 0.97, v.mean()  # the oracle: 0.9515 on codewords 0..3999
     assert 10 < it.mean() < 16, it.mean()
     H = _H(G)
     for b0 in (0, B // 2 - 2048, B - 4096):
