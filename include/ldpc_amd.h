@@ -106,7 +106,7 @@ typedef struct ldpc_schedule {
     int32_t flags_set;   /* LDPC_SCHED_* bits whose value is taken from `flags`; the others keep the default */
     int32_t flags;
     int32_t group_tiles; /* grouped schedule: 64-codeword tiles per check/variable launch
-                            (0 = default: 3, 4 for compressed min-sum; < 0 = the whole pass) */
+                            (0 = default: 3, 8 for compressed min-sum; < 0 = the whole pass) */
     int32_t var_cpw;     /* columns per variable-phase wavefront: 1, 2, 4 or 8 (3: compressed min-sum only;
                             0 = default: 2 for coded input in the resident pool or the compressed
                             min-sum, else 4) */

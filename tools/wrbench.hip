@@ -5,9 +5,9 @@
 //   CSR order (today): the variable kernel scatters a column's 8 segments of
 //     512 B to random rows; the check kernel reads a row's 72 segments
 //     contiguously (36 KB);
-//   CSC order: the variable kernel writes a column's 8 segments contiguously
-//     (4 KB; 16 KB per 4-column wave); the check kernel gathers its 72
-//     segments from random columns.
+//   CSC order (the compressed min-sum's since round 4): the variable kernel
+//     writes a column's 8 segments contiguously (4 KB; 8 KB per 2-column
+//     wave); the check kernel gathers its 72 segments from random columns.
 // Prints GB/s of moved bytes per pattern, nontemporal and plain.
 //
 //   hipcc --offload-arch=gfx950 -O3 -o tools/wrbench tools/wrbench.hip
@@ -119,6 +119,8 @@ int main(int argc, char** argv)
     run_w("write 32 contiguous segments / wave, nt", write_segs<32, true>, 32, ident);
     run_w("write 32 contiguous segments / wave, plain", write_segs<32, false>, 32, ident);
     run_w("write 8 contiguous segments / wave, nt", write_segs<8, true>, 8, ident);
+    run_w("write 16 contiguous segments / wave, nt", write_segs<16, true>, 16, ident);
+    run_w("write 16 contiguous segments / wave, plain", write_segs<16, false>, 16, ident);
     run_r("read 72 contiguous segments / wave, nt", read_segs<72, true>, 72, ident);
     run_r("read 72 contiguous segments / wave, plain", read_segs<72, false>, 72, ident);
     run_r("read 72 random segments / wave, nt", read_segs<72, true>, 72, rnd);
