@@ -256,10 +256,11 @@ def bound_detail(eng, coded=False) -> str:
 
 def _bound_detail(eng) -> str:
     if eng.msa_compressed:
-        return ("compressed min-sum (DESIGN.md sec. 4.2, 6.1): the check kernel streams its 4-tile group's v2c "
-                "(302 MB, more than the 256 MB Infinity Cache) from HBM; the variable kernel gathers the records and "
-                "meta words from its XCD's L2 and scatters the group's fp64 v2c back to HBM as 512-B nontemporal "
-                "segments, whose measured ceiling (ceiling_measured) bounds it; no MFMA")
+        return ("compressed min-sum (DESIGN.md sec. 4.2, 6.1), v2c in column order: the check kernel gathers its "
+                "8-tile group's v2c (604 MB, more than the 256 MB Infinity Cache) from HBM as 512-B segments; the "
+                "variable kernel gathers the records and meta words from its XCD's L2 (one tile per XCD) and writes "
+                "the group's fp64 v2c back as one contiguous nontemporal run per wave, whose measured ceiling "
+                "(ceiling_measured) bounds it; no MFMA")
     if eng.resident:
         return ("resident in-place pool sized to the 256 MB Infinity Cache: every message byte crosses the L2 -> "
                 "fabric interface once per phase (PMC fabric bytes = 1.02-1.04 x algorithmic), served by HBM and the "
@@ -305,15 +306,20 @@ def roofline(eng, G, st, cw_iters, coded=False, cpw=None) -> dict:
     traffic = round(per_cwi * cw_iters / k_launch) if per_cwi else None
     # measured ceiling of the dominant kernel's access shape: the resident pool's in-place passes
     # (tools/cachebench, profiles/r2/cachebench.txt: one launch per in-place pass of the check kernel's shape
-    # over a 192-224 MB working set), or the compressed min-sum variable kernel's v2c scatter (tools/wrbench,
-    # profiles/r3/wrbench_302MB.txt: 8 random 512-B nontemporal segments per wave over the group's 302 MB)
+    # over a 192-224 MB working set), or the compressed min-sum's column-ordered v2c (tools/wrbench over the
+    # 8-tile group's 604 MB, profiles/r4/wrbench_604MB.txt): the variable kernel's 16 contiguous 512-B
+    # nontemporal store segments per wave, the check kernel's 72 random 512-B nontemporal read segments
     ceiling, ceiling_src = None, None
     if eng.resident:
         ceiling, ceiling_src = 6780.0, ("tools/cachebench: in-place 72 x 512 B per wave, one launch per pass, "
                                         "192-224 MB working set (profiles/r2/cachebench.txt)")
     elif eng.msa_compressed and dom == "variable":
-        ceiling, ceiling_src = 5090.0, ("tools/wrbench: 8 random 512-B nontemporal write segments per wave over "
-                                        "302 MB, the variable kernel's v2c scatter (profiles/r3/wrbench_302MB.txt)")
+        ceiling, ceiling_src = 5244.9, ("tools/wrbench: 16 contiguous 512-B nontemporal write segments per wave "
+                                        "over 604 MB, the variable kernel's column-ordered v2c stores "
+                                        "(profiles/r4/wrbench_604MB.txt)")
+    elif eng.msa_compressed:
+        ceiling, ceiling_src = 6420.4, ("tools/wrbench: 72 random 512-B nontemporal read segments per wave over "
+                                        "604 MB, the check kernel's row gathers (profiles/r4/wrbench_604MB.txt)")
     return {
         "bound": "hbm", "kernel": names[dom], "bound_detail": bound_detail(eng, coded),
         "ceiling_measured": ceiling,
