@@ -402,20 +402,27 @@ def dna272(args, og, threads, max_iter=200):
     # count differences k with the table k * ln49 (ldpc_decode_codes), and the
     # fp64 LLR matrix k * ln49 (ldpc_decode: lattice check + encode on the host)
     k8 = np.ascontiguousarray(k.astype(np.int8))
+    kp = L.host_empty(k8.shape, np.int8)  # the same codes in pinned host memory
+    kp[...] = k8
     table = np.arange(-128, 128, dtype=np.float64) * synth.LLR_UNIT
     assert np.array_equal(table[k8.astype(np.int64) + 128], llr)
     G.decode_codes(k8, table, max_iter=max_iter, post=None)
+    G.decode_codes(kp, table, max_iter=max_iter, post=None)
     G.decode(llr, max_iter=max_iter, post=None)
-    th, tl = [], []
+    th, tp, tl = [], [], []
     for _ in range(15):  # the host leg varies with the box's other tenants: median and min of 15 calls
         t = time.perf_counter()
         h2, _, it2, v2 = G.decode_codes(k8, table, max_iter=max_iter, post=None)
         th.append(time.perf_counter() - t)
         t = time.perf_counter()
+        h4, _, it4, v4 = G.decode_codes(kp, table, max_iter=max_iter, post=None)
+        tp.append(time.perf_counter() - t)
+        t = time.perf_counter()
         h3, _, it3, v3 = G.decode(llr, max_iter=max_iter, post=None)
         tl.append(time.perf_counter() - t)
     assert np.array_equal(h2, hard) and np.array_equal(it2, it)
     assert np.array_equal(h3, hard) and np.array_equal(it3, it) and np.array_equal(v3, v2)
+    assert np.array_equal(h4, hard) and np.array_equal(it4, it) and np.array_equal(v4, v2)
     out = {"workload": f"dna272-bp{max_iter}", "batch": B, "max_iter": max_iter, "input": args.input,
            "value": round(B / el, 1), "unit": "codewords/s", "ms_per_decode_device": round(el * 1e3, 3),
            "mean_iters": round(float(it.mean()), 3), "genie_ok": int((hard == cw).all(axis=1).sum()),
@@ -425,6 +432,10 @@ def dna272(args, og, threads, max_iter=200):
            "host_api_includes": "Graph.decode_codes -> ldpc_decode_codes end to end: the int8 count differences k "
                                 "and the table k*ln49 (decoder.py:314) copied to pinned staging + H2D + decode + "
                                 "packed hard-bit D2H + unpack",
+           "host_api_pinned_ms_median": round(float(np.median(tp)) * 1e3, 3),
+           "host_api_pinned_ms_min": round(float(np.min(tp)) * 1e3, 3),
+           "host_api_pinned_includes": "the same call with the codes in pinned host memory (ldpc_amd.host_empty): "
+                                       "no staging copy, one H2D from the caller's array",
            "host_api_llr_ms_median": round(float(np.median(tl)) * 1e3, 3),
            "host_api_llr_ms_min": round(float(np.min(tl)) * 1e3, 3),
            "host_api_llr_includes": "Graph.decode -> ldpc_decode from the fp64 LLR matrix: host lattice check + "

@@ -496,6 +496,16 @@ static int host_decode(const ldpc_graph* gc, const HostInput& in, int64_t B, int
     auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const size_t N = (size_t)g->h.N;
 
+    // codes in pinned host memory (ldpc_host_alloc, hipHostMalloc, a
+    // registered buffer) cross PCIe straight from the caller's array
+    bool codes_pinned = false;
+    if (in.codes) {
+        hipPointerAttribute_t a0{}, a1{};
+        codes_pinned = hipPointerGetAttributes(&a0, in.codes) == hipSuccess && a0.type == hipMemoryTypeHost &&
+                       hipPointerGetAttributes(&a1, in.codes + (size_t)B * N - 1) == hipSuccess &&
+                       a1.type == hipMemoryTypeHost;
+        (void)hipGetLastError();  // pageable memory: the attribute query's error is not sticky
+    }
     std::vector<int> rcs(devs.size(), LDPC_OK);
     std::vector<std::string> msgs(devs.size());
     auto work = [&](size_t di) {
@@ -540,7 +550,9 @@ static int host_decode(const ldpc_graph* gc, const HostInput& in, int64_t B, int
                 // pieces (each crossing while the next is copied)
                 const int8_t* src = in.codes + (size_t)c0(c) * N;
                 if (c >= 2) LDPC_HIP(hipStreamWaitEvent(S.copy, S.ev_dec[k], 0));
-                const int64_t pieces = std::min<int64_t>(4, Bc);
+                const int64_t pieces = codes_pinned ? 0 : std::min<int64_t>(4, Bc);
+                if (codes_pinned)
+                    LDPC_HIP(hipMemcpyAsync(S.d_code[k], src, (size_t)Bc * N, hipMemcpyHostToDevice, S.copy));
                 for (int64_t pc = 0; pc < pieces; pc++) {
                     const int64_t p0 = Bc * pc / pieces, p1 = Bc * (pc + 1) / pieces;
                     parallel_rows(W, p1 - p0, [&](int64_t r0, int64_t r1) {
@@ -837,6 +849,20 @@ int ldpc_engine_stats(ldpc_engine* e, ldpc_kernel_stats* out)
         out->sampled[c] = e->e->sampled[c];
         out->ms[c] = e->e->ms[c];
     }
+    return LDPC_OK;
+}
+
+void* ldpc_host_alloc(size_t bytes)
+{
+    void* p = nullptr;
+    hipError_t e = hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault);
+    if (e != hipSuccess) { set_error(std::string("hipHostMalloc: ") + hipGetErrorString(e)); return nullptr; }
+    return p;
+}
+
+int ldpc_host_free(void* p)
+{
+    if (p) LDPC_HIP(hipHostFree(p));
     return LDPC_OK;
 }
 

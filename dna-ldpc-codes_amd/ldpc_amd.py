@@ -135,7 +135,7 @@ EXPORTS = [
     "ldpc_decode_codes",
     "ldpc_engine_create", "ldpc_engine_create_ex", "ldpc_engine_info", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
     "ldpc_engine_decode_codes", "ldpc_engine_gen_bsc", "ldpc_engine_gen_bsc_codes", "ldpc_engine_set_params", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
-    "ldpc_dev_memcpy", "ldpc_dna_llr", "ldpc_dna_edit_distance", "ldpc_write_soft_files", "ldpc_py_float_repr",
+    "ldpc_dev_memcpy", "ldpc_host_alloc", "ldpc_host_free", "ldpc_dna_llr", "ldpc_dna_edit_distance", "ldpc_write_soft_files", "ldpc_py_float_repr",
 ]
 
 
@@ -192,6 +192,9 @@ def lib():
         L.ldpc_engine_profile.argtypes = [vp, i32]
         L.ldpc_engine_set_params.argtypes = [vp, i32, dbl, i32, C.c_uint64]
         L.ldpc_engine_stats.argtypes = [vp, C.POINTER(KernelStats)]
+        L.ldpc_host_alloc.argtypes = [C.c_size_t]
+        L.ldpc_host_alloc.restype = vp
+        L.ldpc_host_free.argtypes = [vp]
         L.ldpc_dev_malloc.argtypes = [i32, C.c_size_t]
         L.ldpc_dev_malloc.restype = vp
         L.ldpc_dev_free.argtypes = [i32, vp]
@@ -501,6 +504,21 @@ def _schedule_kw(schedule) -> dict:
         kw.update({k: getattr(schedule, k) for k in SCHED_FIELDS if getattr(schedule, k)})
         return kw
     return dict(schedule)
+
+
+def host_empty(shape, dtype=np.int8) -> np.ndarray:
+    """A numpy array in pinned host memory (ldpc_host_alloc), freed with the
+    array.  Graph.decode_codes sends such an input across PCIe without a
+    staging copy."""
+    import weakref
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape)) * dt.itemsize
+    p = lib().ldpc_host_alloc(max(n, 1))
+    if not p:
+        raise LdpcError(LDPC_ERR_DEVICE, (lib().ldpc_last_error() or b"").decode())
+    buf = (C.c_char * max(n, 1)).from_address(p)
+    weakref.finalize(buf, lib().ldpc_host_free, p)
+    return np.frombuffer(buf, dt, count=int(np.prod(shape))).reshape(shape)
 
 
 # ---------------------------------------------------------------------------

@@ -298,6 +298,13 @@ int ldpc_engine_set_params(ldpc_engine *e, int32_t msa_precision, double msa_ste
 int ldpc_engine_info(ldpc_engine *e, int64_t *cap, int64_t *group_tiles, int32_t *flags);
 int ldpc_engine_stats(ldpc_engine *e, ldpc_kernel_stats *out);
 
+/* Pinned (page-locked) host memory.  Host-buffer inputs that live in it cross
+ * PCIe straight from the caller's array (ldpc_decode_codes: no staging
+ * copy); any other host memory is staged through the library's own pinned
+ * buffers. */
+void *ldpc_host_alloc(size_t bytes);
+int ldpc_host_free(void *p);
+
 /* Device buffers for callers without their own HIP allocator (bench, tests). */
 enum { LDPC_H2D = 0, LDPC_D2H = 1, LDPC_D2D = 2 };
 void *ldpc_dev_malloc(int32_t device, size_t bytes);

@@ -271,3 +271,20 @@ def test_host_decode_codes_errors(G):
         G.decode_codes(k, _table()[:100], max_iter=5)
     h, p, it, v = G.decode_codes(k[0], _table(), max_iter=5, post=None)  # 1-D: one codeword
     assert h.shape == (G.N,) and p is None
+
+
+def test_host_decode_codes_pinned_input(G, codewords):
+    """Codes in pinned host memory (ldpc_amd.host_empty / ldpc_host_alloc)
+    cross PCIe straight from the caller's array: the same results as from
+    pageable memory, over several chunks and devices too."""
+    import ldpc_amd as L
+    llr = synth.dna_like_llrs(codewords, seed=22, reads=58000)[:200]
+    k = np.rint(llr / synth.LLR_UNIT).astype(np.int8)
+    kp = L.host_empty(k.shape, np.int8)
+    kp[...] = k
+    for kw in ({}, dict(chunk=64, devices=[0, 0])):
+        a = G.decode_codes(k, _table(), max_iter=60, post="ratio", **kw)
+        b = G.decode_codes(kp, _table(), max_iter=60, post="ratio", **kw)
+        for x, y in zip(a, b):
+            assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+    del kp
