@@ -288,3 +288,23 @@ def test_host_decode_codes_pinned_input(G, codewords):
         for x, y in zip(a, b):
             assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
     del kp
+
+
+@pytest.mark.timeout(200)
+def test_host_decode_codes_several_transfer_chunks(G, codewords):
+    """More codewords than one PCIe transfer chunk (4096): the codes go
+    through the double-buffered chunk pipeline (the next chunk copied while
+    the previous decodes), pageable and pinned, BP and min-sum -- equal to
+    ldpc_decode on the LLRs."""
+    import ldpc_amd as L
+    B = 4096 + 300
+    llr = synth.bsc_llrs(codewords, 0, B, seed=31, p=0.004)
+    k = np.rint(llr / synth.LLR_UNIT).astype(np.int8)
+    kp = L.host_empty(k.shape, np.int8)
+    kp[...] = k
+    for algo in ("bp", "msa"):
+        ref = G.decode(llr, max_iter=20, algo=algo, post=None, schedule=dict(lr_table=False))
+        for src in (k, kp):
+            out = G.decode_codes(src, _table(), max_iter=20, algo=algo, post=None)
+            assert np.array_equal(out[0], ref[0]) and np.array_equal(out[2], ref[2]) and np.array_equal(out[3], ref[3])
+    del kp
