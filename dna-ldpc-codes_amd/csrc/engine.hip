@@ -51,6 +51,10 @@ constexpr int32_t kDefaultSynBlocks = 32;     // continuous-mode syndrome blocks
 constexpr int64_t kMsaPool = 1024;            // compressed min-sum lanes (scattered v2c stores: small pool)
 constexpr int64_t kResAutoMaxTiles = 4;       // explicit pools above this: grouped unless RESIDENT is set
 constexpr int kProbes = 4;                    // placement probe: candidate scratch allocations timed at init
+#ifndef LDPC_MSA_RB
+#define LDPC_MSA_RB 0
+#endif
+constexpr bool kMsaRowBlockMajor = LDPC_MSA_RB != 0;  // compressed min-sum v2c: row-block-major column order (A/B)
 constexpr int32_t kDefaultFlags = LDPC_SCHED_NONTEMPORAL | LDPC_SCHED_CONTINUOUS | LDPC_SCHED_MSA_COMPRESSED |
                                   LDPC_SCHED_RESIDENT | LDPC_SCHED_FIRST_FROM_PRIOR | LDPC_SCHED_LR_TABLE;
 constexpr int32_t kAllFlags = kDefaultFlags | LDPC_SCHED_DEBUG_NO_DRAIN;
@@ -224,10 +228,22 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         for (size_t q = 0; q < er.size(); q++)
             er[q] = ((uint32_t)g->edge_row[(size_t)g->col_edge[q]] << dev::MSA_ER_SHIFT) | (uint32_t)g->col_edge[q];
         if ((rc = upload(&d_col_er, er))) return rc;
-        // CSR edge -> its CSC position: the compressed min-sum keeps v2c in
-        // column order (contiguous variable-phase stores, gathered check reads)
+        // CSR edge -> its v2c position: the compressed min-sum keeps v2c in
+        // column order (contiguous variable-phase stores, gathered check
+        // reads), edge s of column j at j * DV + s -- or, row-block-major,
+        // at s * N + j when edge s of every column lies in row block s
+        // (array codes such as the DNA code's RS-LDPC H: M = DV blocks of
+        // M / DV rows), so a row's gathers stay inside one N-segment region
+        const int dv = g->dv_max;
+        bool rb = kMsaRowBlockMajor && g->M % dv == 0;
+        for (int32_t j = 0; rb && j < g->N; j++)
+            for (int s2 = 0; rb && s2 < dv; s2++)
+                rb = g->edge_row[(size_t)g->col_edge[(size_t)j * dv + s2]] / (g->M / dv) == s2;
+        msa_pa = rb ? 1 : dv;
+        msa_pb = rb ? g->N : 1;
         std::vector<int32_t> pos(g->col_edge.size());
-        for (size_t q = 0; q < pos.size(); q++) pos[(size_t)g->col_edge[q]] = (int32_t)q;
+        for (size_t q = 0; q < pos.size(); q++)
+            pos[(size_t)g->col_edge[q]] = (int32_t)(q / dv) * msa_pa + (int32_t)(q % dv) * msa_pb;
         if ((rc = upload(&d_row_pos, pos))) return rc;
     }
     if (g->regular_dc && g->dc_max > 0) {
@@ -536,7 +552,7 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         const uint16_t* meta = msa_meta(scratch, c2v_tiles, M);
 #define VAR_MSA_C3(CONT, CPW, NT, PC)                                                                                \
     klaunch((k_var_msa_c<72, 8, CONT, CPW, NT, PC>), dim3(nb), dim3(256), 0, s, rec, meta, v2c, prior, hard, d_sgn, \
-            active, d_col_er, pt, N, M, E, t0, (uint32_t)gt, rf)
+            active, d_col_er, pt, N, M, E, t0, (uint32_t)gt, msa_pa, msa_pb, rf)
 #define VAR_MSA_C2(CONT, CPW, NT)                                   \
     do {                                                            \
         if (CONT && rf.in_code) VAR_MSA_C3(CONT, CPW, NT, CONT);    \
@@ -603,7 +619,7 @@ int Engine::run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_i
     const dim3 g_cols_all((N + 3) / 4, (unsigned)tiles);
 
     LAUNCH(K_INIT, klaunch(k_init, g_init, blk, 0, stream, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, msa, Bc, N,
-                           E, d_col_ptr, d_col_edge, prior, v2c, hard, active, iters, valid, d_sgn));
+                           E, d_col_ptr, d_col_edge, prior, v2c, hard, active, iters, valid, d_sgn, msa_pa, msa_pb));
     for (int32_t n = 0;; n++) {
         if (reg_rowT && g->dc_max == 72)
             LAUNCH(K_SYN, klaunch(k_syndrome<72>, dim3((unsigned)tiles), dim3(1024), 0, stream, hard, active,

@@ -84,7 +84,8 @@ struct Engine {
     int32_t* d_col_ptr = nullptr;
     int32_t* d_col_edge = nullptr;
     uint32_t* d_col_er = nullptr;  // [E] (row << 18) | edge id of CSC position q (MSA-C record lookups)
-    int32_t* d_row_pos = nullptr;  // [E] CSC position of CSR edge e (MSA-C: v2c in column order)
+    int32_t* d_row_pos = nullptr;  // [E] v2c position of CSR edge e (MSA-C: v2c in column order)
+    int32_t msa_pa = 8, msa_pb = 1;  // MSA-C: edge s of column j at j * msa_pa + s * msa_pb
     // decoder state
     double* v2c = nullptr;
     double* c2v = nullptr;

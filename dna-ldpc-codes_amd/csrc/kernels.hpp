@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void k_init(const double* __restrict__ in, int
                                               double* __restrict__ prior, double* __restrict__ v2c,
                                               uint64_t* __restrict__ hard, uint64_t* __restrict__ active,
                                               int32_t* __restrict__ iters, uint8_t* __restrict__ valid,
-                                              uint8_t* __restrict__ sgn)
+                                              uint8_t* __restrict__ sgn, int32_t vpa, int32_t vpb)
 {
     __shared__ double s[TILE][TILE + 1];
     const int lane = lane_id(), w = wave_id();
@@ -288,8 +288,10 @@ __global__ __launch_bounds__(256) void k_init(const double* __restrict__ in, int
         }
         prior[((size_t)t * N + j) * TILE + lane] = pv;
         const int32_t a = col_ptr[j], e1 = col_ptr[j + 1];
-        // (the compressed min-sum -- sgn set -- keeps v2c in column order)
-        for (int32_t q = a; q < e1; ++q) v2c[((size_t)t * E + (sgn ? q : col_edge[q])) * TILE + lane] = m;
+        // (the compressed min-sum -- sgn set -- keeps v2c in column order:
+        // edge s of column j at j * vpa + s * vpb, see k_var_msa_c)
+        for (int32_t q = a; q < e1; ++q)
+            v2c[((size_t)t * E + (sgn ? j * vpa + (q - a) * vpb : col_edge[q])) * TILE + lane] = m;
         // compressed min-sum without codes: sign bits of the stored v2c (all edges alike)
         if (sgn) sgn[((size_t)t * N + j) * TILE + lane] = (m >= 0) ? 0u : 0xffu;
         const uint64_t hm = __ballot(h && inb);
@@ -1126,7 +1128,8 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
                                                    double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                    uint8_t* __restrict__ sgn, const uint64_t* __restrict__ active,
                                                    const uint32_t* __restrict__ col_er, double* __restrict__ post,
-                                                   int32_t N, int32_t M, int64_t E, int64_t t0, uint32_t gt, Refill rf)
+                                                   int32_t N, int32_t M, int64_t E, int64_t t0, uint32_t gt,
+                                                   int32_t vpa, int32_t vpb, Refill rf)
 {
     const int lane = lane_id();
     const uint32_t ty = blockIdx.x % gt;
@@ -1283,9 +1286,11 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             uint32_t sbn = 0;
 #pragma unroll
             for (int s = 0; s < DV; ++s) {
-                // v2c in column order: the wave's CPW x DV stores are one contiguous run
+                // v2c in column order: edge s of column j at j * vpa + s * vpb
+                // (vpa = DV, vpb = 1: the wave's stores are one contiguous run;
+                // vpa = 1, vpb = N: row-block-major, one run per row block)
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, dv[s]), rv2c, lane * 8,
-                                                      ((j0 + c) * DV + s) * (TILE * 8), NT ? kBufNT : 0);
+                                                      ((j0 + c) * vpa + s * vpb) * (TILE * 8), NT ? kBufNT : 0);
                 sbn |= (dv[s] >= 0 ? 0u : 1u) << s;
             }
             sgn[pj] = (uint8_t)sbn;
