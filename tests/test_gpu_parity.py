@@ -465,3 +465,27 @@ def test_single_fill_first_check_from_prior(gpu, G, og, codewords):
     ref_h, _, ref_it, ref_v = og.decode_batch(llr, 100, algo=0, threads=8, want_post=False)
     assert np.array_equal(d_i.download(np.empty(B, np.int32)), ref_it)
     assert np.array_equal(d_h.download(np.empty((B, N), np.uint8)), ref_h)
+
+
+@pytest.mark.timeout(240)
+def test_min_sum_compressed_on_rows_permuted(gpu, G, oracle_mod, codewords, tmp_path):
+    """The DNA code with its rows permuted: still (72, 8)-regular, so the
+    compressed min-sum runs, but edge s of a column no longer lies in row
+    block s, so its v2c takes the plain column order instead of the
+    row-block-major one (engine.hip); both layouts are exercised against the
+    oracle, over several fills of the lane pool."""
+    rp, ci, _, _ = G.edges()
+    rows = np.repeat(np.arange(G.M), np.diff(rp))
+    perm = np.random.default_rng(9).permutation(G.M)
+    path = tmp_path / "dna_rows_permuted.pchk"
+    _write_pchk(path, G.M, G.N, perm[rows].tolist(), ci.tolist())
+    og2 = oracle_mod.OracleGraph(str(path))
+    G2 = gpu.Graph(str(path))
+    assert (G2.dc, G2.dv, G2.regular_dc, G2.regular_dv) == (72, 8, True, True)
+    llr = synth.bsc_llrs(codewords, 0, 1500, seed=41, p=0.002)
+    sel = np.r_[0:40, 700:730, 1460:1500]
+    h, p, it, v = G2.decode(llr, max_iter=30, algo="msa", post="llr")
+    rh, rp_, rit, rv = og2.decode_batch(llr[sel], 30, algo=1, post_mode=0, threads=8)
+    assert np.array_equal(h[sel], rh) and np.array_equal(it[sel], rit) and np.array_equal(v[sel], rv.astype(bool))
+    assert np.array_equal(p[sel].view(np.uint64), rp_.view(np.uint64))
+    assert len(np.unique(it)) > 3
