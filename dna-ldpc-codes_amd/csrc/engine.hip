@@ -51,10 +51,7 @@ constexpr int32_t kDefaultSynBlocks = 32;     // continuous-mode syndrome blocks
 constexpr int64_t kMsaPool = 1024;            // compressed min-sum lanes (scattered v2c stores: small pool)
 constexpr int64_t kResAutoMaxTiles = 4;       // explicit pools above this: grouped unless RESIDENT is set
 constexpr int kProbes = 4;                    // placement probe: candidate scratch allocations timed at init
-#ifndef LDPC_MSA_RB
-#define LDPC_MSA_RB 0
-#endif
-constexpr bool kMsaRowBlockMajor = LDPC_MSA_RB != 0;  // compressed min-sum v2c: row-block-major column order (A/B)
+
 constexpr int32_t kDefaultFlags = LDPC_SCHED_NONTEMPORAL | LDPC_SCHED_CONTINUOUS | LDPC_SCHED_MSA_COMPRESSED |
                                   LDPC_SCHED_RESIDENT | LDPC_SCHED_FIRST_FROM_PRIOR | LDPC_SCHED_LR_TABLE;
 constexpr int32_t kAllFlags = kDefaultFlags | LDPC_SCHED_DEBUG_NO_DRAIN;
@@ -235,7 +232,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         // (array codes such as the DNA code's RS-LDPC H: M = DV blocks of
         // M / DV rows), so a row's gathers stay inside one N-segment region
         const int dv = g->dv_max;
-        bool rb = kMsaRowBlockMajor && g->M % dv == 0;
+        bool rb = g->M % dv == 0;  // (round 4 A/B: +1.1 %, profiles/r4/rb/)
         for (int32_t j = 0; rb && j < g->N; j++)
             for (int s2 = 0; rb && s2 < dv; s2++)
                 rb = g->edge_row[(size_t)g->col_edge[(size_t)j * dv + s2]] / (g->M / dv) == s2;
