@@ -366,7 +366,14 @@ class Graph:
         table_kind=IN_LR and BP its LR) -- the DNA stage's count differences
         with table k * ln((1-eps)/eps) (decoder.py:314), ldpc_decode_codes.
         Same outputs as decode(table[codes + 128])."""
-        x = np.ascontiguousarray(codes, dtype=np.int8)
+        c = np.asarray(codes)
+        if c.dtype != np.int8:
+            # no silent wrap-around or truncation of the caller's codes
+            if not np.issubdtype(c.dtype, np.integer):
+                raise TypeError(f"codes must be integers (got {c.dtype})")
+            if c.size and (int(c.min()) < -128 or int(c.max()) > 127):
+                raise ValueError("codes outside the int8 range [-128, 127]")
+        x = np.ascontiguousarray(c, dtype=np.int8)
         t = np.ascontiguousarray(table, dtype=np.float64)
         if t.shape != (256,):
             raise ValueError("the code table has 256 entries (code + 128)")

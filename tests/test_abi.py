@@ -203,3 +203,19 @@ def test_graph_blocks_array_structure(L):
     assert (Q, rb, cb) == (32, 4, 16) and np.array_equal(cls, np.arange(16 * 32) // 32)
     irr = L.Graph.from_edges(4, 6, [0, 0, 1, 1, 2, 3], [0, 1, 2, 3, 4, 5])
     assert irr.blocks() is None
+
+
+def test_decode_codes_rejects_codes_off_int8(L):
+    """Graph.decode_codes checks the caller's codes before any device call:
+    wider integer codes outside [-128, 127] and non-integer arrays raise
+    instead of wrapping or truncating (in range, any integer dtype is taken)."""
+    G = L.Graph(PCHK)
+    table = np.arange(-128, 128, dtype=np.float64)
+    with pytest.raises(ValueError, match="int8 range"):
+        G.decode_codes(np.full((2, G.N), 200, np.int16), table, max_iter=1)
+    with pytest.raises(ValueError, match="int8 range"):
+        G.decode_codes(np.full((2, G.N), -129, np.int64), table, max_iter=1)
+    with pytest.raises(TypeError, match="integers"):
+        G.decode_codes(np.zeros((2, G.N), np.float64), table, max_iter=1)
+    with pytest.raises(ValueError, match="256 entries"):
+        G.decode_codes(np.zeros((2, G.N), np.int32), table[:10], max_iter=1)
