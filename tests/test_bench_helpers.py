@@ -56,3 +56,29 @@ def test_roofline_moved_bytes():
     assert rm["frac_of_measured_ceiling"] == round(rm["achieved_moved"] / rm["ceiling_measured"], 4)
     rf = b.roofline(_eng(msa_compressed=True, resident=False, nontemporal=True, algo=1), G, st, cw_iters, coded=False)
     assert rf["achieved_moved"] == rf["achieved"]
+
+
+def test_kernel_names_match_the_committed_trace_and_traffic_table():
+    """bench.kernel_names gives the template instantiations the engine
+    launches in the default line (config 3: resident BP with coded priors;
+    config 5: continuous compressed min-sum with coded priors): each must be a
+    kernel of the committed rocprofv3 trace of that command and have an entry
+    in the PMC traffic table bench.py reads for roofline.traffic, so a
+    renamed template cannot silently drop the line's `traffic`."""
+    import csv
+    import glob
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_summary import short
+    b = _bench()
+    final = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "final", "default_bench_rocprofv3_kernel_stats.csv")))[-1]
+    traced = {short(r["Name"]) for r in csv.DictReader(open(final))}
+    table = json.load(open(sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))[-1]))
+    known = set(table["per_cw_iter_by_instantiation"])
+    bp = b.kernel_names(_eng(), "bp", coded=True)
+    msa = b.kernel_names(_eng(msa_compressed=True, resident=False, nontemporal=True, algo=1), "msa", coded=True)
+    for names in (bp, msa):
+        for kind, name in names.items():
+            assert name in traced, (kind, name)
+            assert name in known, (kind, name)
