@@ -260,8 +260,7 @@ def _bound_detail(eng) -> str:
                 "8-tile group's v2c (604 MB, more than the 256 MB Infinity Cache) from HBM as 512-B segments; the "
                 "variable kernel gathers the records and meta words from its XCD's L2 (one tile per XCD) and writes "
                 "the group's fp64 v2c back nontemporally (row-block-major: per wave one 1-KB run into each of the 8 "
-                "row-block streams), at the measured store ceiling's bound (ceiling_measured: the faster of the "
-                "measured 16-contiguous and 8-scattered segment shapes); no MFMA")
+                "row-block streams), bounded by that store shape's measured ceiling (ceiling_measured); no MFMA")
     if eng.resident:
         return ("resident in-place pool sized to the 256 MB Infinity Cache: every message byte crosses the L2 -> "
                 "fabric interface once per phase (PMC fabric bytes = 1.02-1.04 x algorithmic), served by HBM and the "
@@ -308,21 +307,21 @@ def roofline(eng, G, st, cw_iters, coded=False, cpw=None) -> dict:
     # measured ceiling of the dominant kernel's access shape: the resident pool's in-place passes
     # (tools/cachebench, profiles/r2/cachebench.txt: one launch per in-place pass of the check kernel's shape
     # over a 192-224 MB working set), or the compressed min-sum's column-ordered v2c (tools/wrbench over the
-    # 8-tile group's 604 MB, profiles/r4/wrbench_604MB.txt): for the variable kernel's stores (16 segments
-    # per wave in eight 2-segment runs, row-block-major) the faster of the measured 16-contiguous (5.24 TB/s)
-    # and 8-scattered (5.13 TB/s) nontemporal store shapes; the check kernel's 72 random 512-B nontemporal
-    # read segments
+    # 8-tile group's 604 MB): the variable kernel's stores and the check kernel's row gathers in exactly
+    # the kernels' wave order over the row-block-major v2c of the DNA code (tools/wrbench "rb" shapes,
+    # profiles/r4/wrbench_rb_604MB*.txt; the faster of two runs)
     ceiling, ceiling_src = None, None
     if eng.resident:
         ceiling, ceiling_src = 6780.0, ("tools/cachebench: in-place 72 x 512 B per wave, one launch per pass, "
                                         "192-224 MB working set (profiles/r2/cachebench.txt)")
     elif eng.msa_compressed and dom == "variable":
-        ceiling, ceiling_src = 5244.9, ("tools/wrbench: 16 contiguous 512-B nontemporal write segments per wave "
-                                        "over 604 MB (8 scattered: 5134.3), the nearest measured shapes to the "
-                                        "variable kernel's row-block-major v2c stores (profiles/r4/wrbench_604MB.txt)")
+        ceiling, ceiling_src = 5079.6, ("tools/wrbench: the variable kernel's nontemporal v2c stores in its own "
+                                        "wave order over the row-block-major 604 MB group "
+                                        "(profiles/r4/wrbench_rb_604MB_run2.txt)")
     elif eng.msa_compressed:
-        ceiling, ceiling_src = 6420.4, ("tools/wrbench: 72 random 512-B nontemporal read segments per wave over "
-                                        "604 MB, the check kernel's row gathers (profiles/r4/wrbench_604MB.txt)")
+        ceiling, ceiling_src = 6876.5, ("tools/wrbench: the check kernel's nontemporal row gathers in its own "
+                                        "wave order over the row-block-major 604 MB group "
+                                        "(profiles/r4/wrbench_rb_604MB.txt)")
     return {
         "bound": "hbm", "kernel": names[dom], "bound_detail": bound_detail(eng, coded),
         "ceiling_measured": ceiling,

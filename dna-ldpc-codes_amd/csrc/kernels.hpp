@@ -1064,25 +1064,39 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
         x[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv2c, lane * 8, pos[k] * (TILE * 8),
                                                                                NT ? kBufNT : 0));
     // one pass: min1 with its FIRST index, min2 = minimum over the other
-    // indices (a tie with min1 gives min2 == min1), NaN never compares less
+    // indices (a tie with min1 gives min2 == min1), NaN never compares less.
+    // Without NaN as min / max (each returns one operand, bit for bit):
+    //   m2 = min(m2, max(m1, a)), m1 = min(m1, a), i1 by the strict a < m1
+    // -- the selects below, in a third of the VALU work; the sign parity
+    // and the NaN flag as lane masks.  A lane with a NaN redoes the row with
+    // the selects (max(m1, NaN) would drop the NaN and shrink m2).
     double m1 = __builtin_inf(), m2 = __builtin_inf();
     int i1 = -1;
-    uint32_t negb[(DC + 31) / 32] = {};
+    bool neg = false, anynan = false;
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
         const double a = __builtin_fabs(x[k]);
-        negb[k / 32] |= ((x[k] >= 0) ? 0u : 1u) << (k % 32);
-        // if (a < m1) { m2 = m1; m1 = a; i1 = k; } else if (a < m2) m2 = a;
-        // as selects (no per-edge lane-masked branch); NaN compares false
-        const bool lt1 = a < m1, lt2 = a < m2;
-        m2 = lt1 ? m1 : (lt2 ? a : m2);
-        m1 = lt1 ? a : m1;
-        i1 = lt1 ? k : i1;
+        neg ^= !(x[k] >= 0);
+        anynan |= __builtin_isnan(a);
+        i1 = (a < m1) ? k : i1;
+        m2 = __builtin_fmin(m2, __builtin_fmax(m1, a));
+        m1 = __builtin_fmin(m1, a);
     }
-    uint32_t neg = 0;
+    if (__builtin_expect(__ballot(anynan) != 0ull, 0) && anynan) {
+        m1 = __builtin_inf();
+        m2 = __builtin_inf();
+        i1 = -1;
 #pragma unroll
-    for (int w = 0; w < (DC + 31) / 32; ++w) neg ^= (uint32_t)__builtin_popcount(negb[w]);
-    neg &= 1u;
+        for (int k = 0; k < DC; ++k) {
+            // if (a < m1) { m2 = m1; m1 = a; i1 = k; } else if (a < m2) m2 = a;
+            // as selects (no per-edge lane-masked branch); NaN compares false
+            const double a = __builtin_fabs(x[k]);
+            const bool lt1 = a < m1, lt2 = a < m2;
+            m2 = lt1 ? m1 : (lt2 ? a : m2);
+            m1 = lt1 ? a : m1;
+            i1 = lt1 ? k : i1;
+        }
+    }
     const double a0 = __builtin_fabs(x[0]), a1 = __builtin_fabs(x[1]);
     const bool nan0 = __builtin_isnan(a0), nan1 = __builtin_isnan(a1);
     double* __restrict__ r = rec + ((size_t)blockIdx.y * M + row) * (MSA_REC_PLANES * TILE) + lane;
@@ -1091,7 +1105,7 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     if (nan0) r[2 * TILE] = a0;
     if (nan1) r[3 * TILE] = a1;
     meta[((size_t)blockIdx.y * M + row) * TILE + lane] =
-        (uint16_t)((neg << 15) | ((nan1 ? 1u : 0u) << 14) | ((nan0 ? 1u : 0u) << 13) |
+        (uint16_t)(((neg ? 1u : 0u) << 15) | ((nan1 ? 1u : 0u) << 14) | ((nan0 ? 1u : 0u) << 13) |
                    (i1 < 0 ? MSA_META_NONE : ((uint32_t)(row * DC + i1) & MSA_META_ID)));
 }
 

@@ -8,12 +8,20 @@
 //   CSC order (the compressed min-sum's since round 4): the variable kernel
 //     writes a column's 8 segments contiguously (4 KB; 8 KB per 2-column
 //     wave); the check kernel gathers its 72 segments from random columns.
+//   row-block-major (the compressed min-sum's on the DNA code since round 4,
+//     at a 604 MB size = 8 tiles of the DNA code, E = 147456 segments each):
+//     edge s of column j at s * N + j of its tile; the variable kernel's
+//     wave order (1-D grid, block L -> tile L % 8, two columns per wave,
+//     stores in (column, s) order) and the check kernel's (grid (M / 4, 8),
+//     row r of row block s = r / 256 gathering its 72 columns ascending, a
+//     random partition of the N columns into the block's 256 rows).
 // Prints GB/s of moved bytes per pattern, nontemporal and plain.
 //
 //   hipcc --offload-arch=gfx950 -O3 -o tools/wrbench tools/wrbench.hip
 //   tools/wrbench [MB]
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -102,6 +110,45 @@ int main(int argc, char** argv)
         std::swap(h[i], h[x % (i + 1)]);
     }
     CK(hipMemcpy(rnd, h.data(), nseg * 4, hipMemcpyHostToDevice));
+    // row-block-major shapes of the DNA code (N = 18432, M = 2048, 8 row blocks), 8 tiles
+    constexpr int NC = 18432, MR = 2048, DV = 8, DC = 72, RB = MR / DV;
+    constexpr size_t ET = (size_t)NC * DV;
+    int *rbw = nullptr, *rbr = nullptr;
+    const bool rb = nseg % ET == 0;
+    if (rb) {
+        const size_t tiles = nseg / ET;
+        std::vector<int> w(nseg), r(nseg);
+        // variable kernel: wave v = block L * 4 + w4; tile L % tiles, columns j0, j0 + 1
+        for (size_t v = 0; v < nseg / 16; v++) {
+            const size_t L = v / 4, w4 = v % 4, ty = L % tiles, cb = L / tiles;
+            const size_t j0 = (cb * 4 + w4) * 2;
+            for (int c = 0; c < 2; c++)
+                for (int sb = 0; sb < DV; sb++) w[v * 16 + c * DV + sb] = (int)(ty * ET + (size_t)sb * NC + j0 + c);
+        }
+        // check kernel: wave v = tile * M + row; row r of block r / RB reads its 72 columns ascending
+        std::vector<int> perm(NC);
+        std::vector<int> cols((size_t)MR * DC);
+        for (int sb = 0; sb < DV; sb++) {
+            for (int j = 0; j < NC; j++) perm[j] = j;
+            for (int j = NC - 1; j > 0; j--) {
+                x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+                std::swap(perm[j], perm[x % (j + 1)]);
+            }
+            for (int u = 0; u < RB; u++) {
+                int* c = cols.data() + ((size_t)sb * RB + u) * DC;
+                for (int k = 0; k < DC; k++) c[k] = perm[u * DC + k];
+                std::sort(c, c + DC);
+            }
+        }
+        for (size_t v = 0; v < nseg / DC; v++) {
+            const size_t t = v / MR, row = v % MR, sb = row / RB;
+            for (int k = 0; k < DC; k++) r[v * DC + k] = (int)(t * ET + sb * NC + (size_t)cols[row * DC + k]);
+        }
+        CK(hipMalloc(&rbw, nseg * 4));
+        CK(hipMalloc(&rbr, nseg * 4));
+        CK(hipMemcpy(rbw, w.data(), nseg * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(rbr, r.data(), nseg * 4, hipMemcpyHostToDevice));
+    }
     const int reps = 10;
     auto run_w = [&](const char* name, auto kern, int SEG, const int* seg) {
         const size_t nw = nseg / SEG;
@@ -125,5 +172,9 @@ int main(int argc, char** argv)
     run_r("read 72 contiguous segments / wave, plain", read_segs<72, false>, 72, ident);
     run_r("read 72 random segments / wave, nt", read_segs<72, true>, 72, rnd);
     run_r("read 72 random segments / wave, plain", read_segs<72, false>, 72, rnd);
+    if (rb) {
+        run_w("write rb, variable kernel's order, nt", write_segs<16, true>, 16, rbw);
+        run_r("read rb, check kernel's order, nt", read_segs<72, true>, 72, rbr);
+    }
     return 0;
 }
