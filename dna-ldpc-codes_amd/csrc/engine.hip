@@ -463,13 +463,14 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
             LAUNCH_ON(s, K_CHECK, klaunch((k_check_bp<72, false, true>), grid, blk, 0, s, v2c, v2c, active, M, E, t0, *rstep));
         return LDPC_OK;
     }
-    if (msa_c) {
+    if (msa_c) {  // 1-D XCD-affine grid (k_check_msa_c)
+        const dim3 g1((unsigned)((M + 3) / 4) * gt);
         if (nt_d)
-            LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, true>), grid, blk, 0, s, v2c, msa_rec(scratch),
-                                          msa_meta(scratch, c2v_tiles, M), active, d_row_pos, M, E, t0));
+            LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, true>), g1, blk, 0, s, v2c, msa_rec(scratch),
+                                          msa_meta(scratch, c2v_tiles, M), active, d_row_pos, M, E, t0, gt));
         else
-            LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, false>), grid, blk, 0, s, v2c, msa_rec(scratch),
-                                          msa_meta(scratch, c2v_tiles, M), active, d_row_pos, M, E, t0));
+            LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa_c<72, false>), g1, blk, 0, s, v2c, msa_rec(scratch),
+                                          msa_meta(scratch, c2v_tiles, M), active, d_row_pos, M, E, t0, gt));
         return LDPC_OK;
     }
     if (reg72) {

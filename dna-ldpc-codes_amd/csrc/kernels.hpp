@@ -1037,18 +1037,22 @@ constexpr int MSA_REC_PLANES = 4;
 constexpr uint32_t MSA_META_ID = 0x7fu;      // meta bits 0-6: low bits of min1's edge id
 constexpr uint32_t MSA_META_NONE = 0x1000u;  // meta bit 12: no min1 (never equals an edge's low bits)
 
-// grid (ceil(M/4), group tiles), block 256: one wave per (row, tile); the
-// v2c group is streamed once (NT: nontemporal loads).
+// 1-D grid of gt * ceil(M/4) blocks, block 256: one wave per (row, tile);
+// block L works on group tile L % gt, so with gt | 8 each XCD writes the
+// records of the one tile whose variable blocks it runs next (k_var_msa_c's
+// mapping) and they are read back from its own L2.  The v2c group is
+// streamed once (NT: nontemporal loads).
 template <int DC, bool NT>
 __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ v2c, double* __restrict__ rec,
                                                      uint16_t* __restrict__ meta, const uint64_t* __restrict__ active,
                                                      const int32_t* __restrict__ row_pos, int32_t M, int64_t E,
-                                                     int64_t t0)
+                                                     int64_t t0, uint32_t gt)
 {
     static_assert(DC >= 2 && DC <= 96, "row degree");
     const int lane = lane_id();
-    const int32_t row = blockIdx.x * 4 + wave_id();
-    const int64_t t = t0 + blockIdx.y;
+    const uint32_t ty = blockIdx.x % gt;
+    const int32_t row = (int32_t)(blockIdx.x / gt) * 4 + wave_id();
+    const int64_t t = t0 + ty;
     const uint64_t act = active[t];
     // whole-line policy (as k_check_msa)
     if (!(row < M && line_occupied(act, lane))) return;
@@ -1099,12 +1103,12 @@ __global__ __launch_bounds__(256) void k_check_msa_c(const double* __restrict__ 
     }
     const double a0 = __builtin_fabs(x[0]), a1 = __builtin_fabs(x[1]);
     const bool nan0 = __builtin_isnan(a0), nan1 = __builtin_isnan(a1);
-    double* __restrict__ r = rec + ((size_t)blockIdx.y * M + row) * (MSA_REC_PLANES * TILE) + lane;
+    double* __restrict__ r = rec + ((size_t)ty * M + row) * (MSA_REC_PLANES * TILE) + lane;
     r[0] = m1;
     r[TILE] = m2;
     if (nan0) r[2 * TILE] = a0;
     if (nan1) r[3 * TILE] = a1;
-    meta[((size_t)blockIdx.y * M + row) * TILE + lane] =
+    meta[((size_t)ty * M + row) * TILE + lane] =
         (uint16_t)(((neg ? 1u : 0u) << 15) | ((nan1 ? 1u : 0u) << 14) | ((nan0 ? 1u : 0u) << 13) |
                    (i1 < 0 ? MSA_META_NONE : ((uint32_t)(row * DC + i1) & MSA_META_ID)));
 }
