@@ -976,8 +976,8 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         if (s >= limit) return overrun(s);
         const uint64_t q = poll_seq++;
         poll_arm(rs.cs, q);
-        LAUNCH(K_SYN, klaunch(k_syndrome_split<72>, dim3((unsigned)syn_blocks, (unsigned)tiles), dim3(256), 0,
-                              stream, M, rs));
+        LAUNCH(K_SYN, klaunch(k_syndrome_split<72>, dim3((unsigned)(syn_blocks * tiles)), dim3(256), 0, stream, M,
+                              rs, (uint32_t)tiles));
         const int64_t gstep = low ? std::max(group_tiles, c2v_tiles) : group_tiles;
         if (ffp && cur_codes && s == 0 && N % 64 == 0) {
             // single fill on codes: step 0 is the transpose of the claimed

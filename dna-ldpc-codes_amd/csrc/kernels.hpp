@@ -1392,11 +1392,15 @@ __global__ __launch_bounds__(256) void k_cont_reset(uint64_t* __restrict__ activ
 // the parts are XOR-combined across lanes, and the rows OR-combined; the
 // tile's last block runs cont_lanes and hands the finished lanes to the
 // variable kernel (Refill::fin), which writes their outputs.
+// 1-D grid of nblk blocks per tile for `tiles` tiles: block L works on tile
+// L % tiles, so with 8 | tiles each XCD gathers the ballots its own variable
+// blocks just wrote (k_var_msa_c's tile-per-XCD mapping) from its L2.
 template <int DC>
-__global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs)
+__global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs, uint32_t tiles)
 {
     constexpr int KP = (DC + 7) / 8;
-    const int64_t t = blockIdx.y;
+    const int64_t t = blockIdx.x % tiles;
+    const uint32_t blk = blockIdx.x / tiles, nblk = gridDim.x / tiles;
     const uint64_t occ = rs.cs.occupied[t];
     const int lane = lane_id();
     int32_t ln0 = 0;
@@ -1409,7 +1413,7 @@ __global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs)
         }
         const uint64_t* __restrict__ h = rs.hard + (size_t)t * rs.N;
         const int part = lane >> 3;
-        for (int32_t r0 = (int32_t)(blockIdx.x * 4 + wave_id()) * 8; r0 < M; r0 += (int32_t)gridDim.x * 32) {
+        for (int32_t r0 = (int32_t)(blk * 4 + wave_id()) * 8; r0 < M; r0 += (int32_t)nblk * 32) {
             const int32_t row = r0 + (lane & 7);
             uint64_t p = 0;
             if (row < M) {
@@ -1429,7 +1433,7 @@ __global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs)
         u |= shfl_xor_u64(u, 2);
         u |= shfl_xor_u64(u, 4);
     }
-    res_arrive(t, occ, u, rs, ln0, b0, gridDim.x);
+    res_arrive(t, occ, u, rs, ln0, b0, nblk);
 }
 
 // hard ballots -> [b][N] u8 (the reference's dblk / dec_*.txt bits)
