@@ -37,6 +37,13 @@ At N = 1 (unless --secondary 0) two driver-timed secondary legs follow the
 headline, each with its own oracle check, under "secondary": config 2 (the
 272-codeword DNA batch through the host API ldpc_decode, median of 15 calls)
 and config 5 (1M codewords, min-sum with early exit, 2 timed steps).
+
+At N > 1, after the headline and every rank's check: rank 0 times the oracle
+on all the host cores it may use while the other ranks wait in a barrier
+(`cpu_baseline`, as at N = 1), and at N = 8 BASELINE config 4 follows as
+"secondary.config4_1m_strong" -- 1M codewords split by dist.shard, 1 warm-up
++ 2 timed decodes (max over ranks), every rank's shard oracle-checked
+(--config4 G forces a G-codeword leg at any N > 1).
 """
 from __future__ import annotations
 
@@ -100,6 +107,10 @@ def parse():
                     help="channel output in HBM: int8 codes + a 256-entry table (default) or fp64 LR / LLR")
     ap.add_argument("--workload", default="bsc", choices=["bsc", "dna272"],
                     help="bsc: SURVEY 8(d) configs 3-5 (default); dna272: config 2, the 272-codeword DNA batch")
+    ap.add_argument("--config4", default="auto",
+                    help="N > 1: BASELINE config 4 as a secondary leg after the headline -- G codewords strong-sharded "
+                         "over the ranks (dist.shard), 1 warm-up + 2 timed decodes, every rank oracle-checked; "
+                         "'auto' (default): G = 1000000 at N = 8 only; an integer G > 0 forces it at any N > 1; 0: off")
     return ap.parse_args()
 
 
@@ -329,7 +340,7 @@ def roofline(eng, G, st, cw_iters, coded=False, cpw=None) -> dict:
         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
         # a physical rate against a physical ceiling: the bytes the kernel moves
-        "frac_of_measured_ceiling": round(achieved_moved / ceiling, 4) if (achieved_moved and ceiling) else None,
+        "frac_moved_of_measured_ceiling": round(achieved_moved / ceiling, 4) if (achieved_moved and ceiling) else None,
         "traffic": traffic,
         "traffic_source": traffic_src,
         "traffic_per_cw_iter": per_cwi,
@@ -569,6 +580,79 @@ def msa_1m(args, og, threads, cw, d_cw):
     return out
 
 
+def config4_total(opt: str, world: int, global_batch: int) -> int:
+    """Codewords of the config-4 leg (0: none): --config4 auto runs BASELINE
+    config 4 -- 1M codewords over 8 GPUs -- in the driver's 8-GPU weak-scaling
+    run; an integer forces that global batch at any N > 1."""
+    if world <= 1:
+        return 0
+    if opt == "auto":
+        return 1_000_000 if world == 8 and global_batch == 0 else 0
+    return max(0, int(opt))
+
+
+def config4_leg(args, L, dist, grp, G, dev, d_cw, cw, og, threads, total):
+    """BASELINE config 4 inside an N > 1 run: `total` codewords (1M at N = 8)
+    split over the ranks by dist.shard -- DNA_main.cpp:629-651 Set_FrameNum's
+    contiguous per-rank frame ranges, with the counters combined as its
+    MPI_Reduce does (:1187-1193) -- on the default BP engine, 1 warm-up + 2
+    timed decodes bracketed by barriers (max over ranks), then every rank
+    checks the head, last rows and random interior rows of its shard against
+    the oracle; the per-rank checks are gathered."""
+    import synth
+    world, rank = grp.world, grp.rank
+    N = G.N
+    b0, B = dist.shard(total, world, rank)
+    eng = L.Engine(G, dev, "bp")
+    d_in, decode = channel(L, eng, args, dev, N, b0, B, d_cw, cw.shape[0], args.p, L.IN_LR)
+    d_hard, d_iters, d_valid = L.DeviceBuffer(dev, B * N), L.DeviceBuffer(dev, B * 4), L.DeviceBuffer(dev, B)
+
+    def step():
+        decode(B, args.max_iter, d_hard.at(0), d_iters.at(0), d_valid.at(0))
+
+    step()
+    eng.sync()
+    steps = 2
+    grp.barrier()
+    t = time.perf_counter()
+    for _ in range(steps):
+        step()
+    eng.sync()
+    el = time.perf_counter() - t
+    grp.barrier()
+    el_max = grp.max(el)
+    iters = d_iters.download(np.empty(B, np.int32))
+    valid = d_valid.download(np.empty(B, np.uint8))
+
+    def llr_fn(start, n):
+        return synth.bsc_llrs(cw, b0 + start, n, seed=args.seed, p=args.p)
+
+    def gpu_out(start, n):
+        return d_hard.download(np.empty((n, N), np.uint8), offset=start * N), iters[start:start + n], \
+            valid[start:start + n]
+
+    n = min(B, max(2, args.check_per_thread * threads))
+    head = n - n // 2
+    tail, inter = tail_and_interior(B, head, n_tail=n // 2, seed=args.seed + 100 + rank)
+    checked, bad, _ = oracle_check(og, llr_fn, gpu_out, 0, args.max_iter, [(0, head), tail, inter], threads)
+    per = grp.gather({"rank": rank, "b0": b0, "B": B, "checked": checked, "mismatches": len(bad),
+                      "first_mismatches": [b0 + k for k in bad[:4]], "threads": threads,
+                      "mean_iters": round(float(iters.mean()), 3),
+                      "rows": {"head": [0, head], "tail": [int(tail[0]), B] if tail.size else None,
+                               "interior": inter.tolist()}})
+    for b in (d_in, d_hard, d_iters, d_valid):
+        b.free()
+    eng.close()
+    return {"workload": f"bsc-p{args.p}-{total // 1000}k-global-bp{args.max_iter}", "global_batch": total,
+            "n_gpus": world, "scaling": "strong", "per_rank": [p["B"] for p in per], "steps": steps,
+            "value": round(total * steps / el_max, 2), "unit": "codewords/s",
+            "ms_per_step": round(el_max / steps * 1e3, 3), "input": args.input,
+            "check": {"checked": sum(p["checked"] for p in per), "mismatches": sum(p["mismatches"] for p in per),
+                      "per_rank": per,
+                      "what": "hard bits, iteration counts and valid flags of the timed decode vs the oracle on "
+                              "every rank's shard: head, last rows (the lane pool's drain), random interior rows"}}
+
+
 def launch_ranks(n: int) -> int:
     """`bench.py --gpus N` run without a launcher: start N ranks under
     torch.distributed.run as a CHILD process (this process has not touched
@@ -723,6 +807,21 @@ def main():
         tail, inter = tail_and_interior(B, head, n_tail=n // 2, seed=args.seed + rank)
         checked, bad, _ = oracle_check(og, llr_fn, gpu_out, a, args.max_iter, [(0, head), tail, inter], threads)
         rows = {"head": [0, head], "tail": [int(tail[0]), B] if tail.size else None, "interior": inter.tolist()}
+    if world > 1 and args.cpu_baseline:
+        # the CPU path timed on the node's host cores in the same run
+        # (north_star): rank 0 alone, on every core it may use, while the
+        # other ranks wait in the barrier; its sample is rank 0's shard head,
+        # checked against the timed decode as well
+        grp.barrier()
+        if rank == 0:
+            cb, (c_cb, bad_cb, rows_cb) = cpu_baseline(args, og, llr_fn, B, gpu_out, cpus)
+            cb["while"] = f"ranks 1..{world - 1} idle in a gloo barrier after their own checks"
+            cb["checked"], cb["mismatches"] = c_cb, len(bad_cb)
+            out["cpu_baseline"] = cb
+            checked += c_cb
+            bad = bad + bad_cb
+            rows = dict(rows, cpu_baseline=rows_cb)
+        grp.barrier()
     per = grp.gather({"rank": rank, "b0": b0, "B": B, "checked": checked, "mismatches": len(bad),
                       "first_mismatches": [b0 + k for k in bad[:4]], "threads": threads, "rows": rows})
     out["check"] = {"checked": sum(p["checked"] for p in per), "mismatches": sum(p["mismatches"] for p in per),
@@ -731,6 +830,19 @@ def main():
                             "every rank's own shard: its head (N = 1: the cpu_baseline sample), its last rows (the "
                             "lane pool's drain) and random interior rows (per_rank[].rows, shard-relative)"}
     mismatches = out["check"]["mismatches"]
+
+    # ---- BASELINE config 4 (N > 1): 1M codewords strong-sharded, after the headline ----
+    c4 = config4_total(args.config4, world, args.global_batch)
+    if c4 > 0 and algo == "bp":
+        for b in (d_in, d_hard, d_iters, d_valid):
+            b.free()
+        eng.close()
+        t = time.perf_counter()
+        leg = config4_leg(args, L, dist, grp, G, dev, d_cw, cw, og, threads, c4)
+        leg["leg_wall_s"] = round(time.perf_counter() - t, 2)
+        out["secondary"] = {"note": "driver-timed after the headline region; not part of value / ms_per_step",
+                            "config4_1m_strong" if c4 == 1_000_000 else "config4_strong": leg}
+        mismatches += leg["check"]["mismatches"]
 
     # ---- secondary legs (N = 1): config 3 on fp64 input, config 5 and config 2, each checked ----
     if world == 1 and args.secondary and args.global_batch == 0 and algo == "bp":

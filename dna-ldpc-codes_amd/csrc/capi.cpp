@@ -496,8 +496,9 @@ static int host_decode(const ldpc_graph* gc, const HostInput& in, int64_t B, int
     auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const size_t N = (size_t)g->h.N;
 
-    // codes in pinned host memory (ldpc_host_alloc, hipHostMalloc, a
-    // registered buffer) cross PCIe straight from the caller's array
+    // codes in pinned host memory (ldpc_host_alloc / hipHostMalloc: mapped
+    // for every device) cross PCIe straight from the caller's array; the
+    // tested case is ldpc_host_alloc memory
     bool codes_pinned = false;
     if (in.codes) {
         hipPointerAttribute_t a0{}, a1{};
@@ -714,10 +715,7 @@ static int host_decode(const ldpc_graph* gc, const HostInput& in, int64_t B, int
         }
         if (rc == LDPC_OK) rc = finish(nch - 1);
         if (api_timing) std::fprintf(stderr, "api shard %zu: %.3f ms\n", di, now() - t_call);
-        if (rc == LDPC_OK && hipStreamSynchronize(E.stream) != hipSuccess) {  // surplus steps of the last decode
-            set_error("hipStreamSynchronize failed");
-            rc = LDPC_ERR_DEVICE;
-        }
+        if (rc == LDPC_OK) rc = E.sync();  // surplus steps of the last decode; a device fault report
         if (rc) { rcs[di] = rc; msgs[di] = ldpc::last_error(); return; }
         g->give(std::move(slot));
     };
@@ -807,9 +805,7 @@ int ldpc_engine_decode_codes(ldpc_engine* e, const int8_t* d_codes, const double
 int ldpc_engine_sync(ldpc_engine* e)
 {
     if (!e) { set_error("null engine"); return LDPC_ERR_ARG; }
-    LDPC_HIP(hipSetDevice(e->e->device));
-    LDPC_HIP(hipStreamSynchronize(e->e->stream));
-    return LDPC_OK;
+    return e->e->sync();
 }
 
 void* ldpc_engine_stream(ldpc_engine* e) { return e ? (void*)e->e->stream : nullptr; }

@@ -54,7 +54,7 @@ constexpr int kProbes = 4;                    // placement probe: candidate scra
 
 constexpr int32_t kDefaultFlags = LDPC_SCHED_NONTEMPORAL | LDPC_SCHED_CONTINUOUS | LDPC_SCHED_MSA_COMPRESSED |
                                   LDPC_SCHED_RESIDENT | LDPC_SCHED_FIRST_FROM_PRIOR | LDPC_SCHED_LR_TABLE;
-constexpr int32_t kAllFlags = kDefaultFlags | LDPC_SCHED_DEBUG_NO_DRAIN;
+constexpr int32_t kAllFlags = kDefaultFlags | LDPC_SCHED_DEBUG_NO_DRAIN | LDPC_SCHED_DEBUG_BAD_LANE;
 
 // flags_set bits of a resolved schedule, outside kAllFlags: resolved, and
 // whether the caller chose the resident pool (the auto-disable rule for
@@ -123,6 +123,7 @@ Engine::~Engine()
     for (auto e : ev_pool) hipEventDestroy(e);
     hipFree(d_fresh); hipFree(d_occ); hipFree(d_lane_b); hipFree(d_lane_n); hipFree(d_ctr);
     if (h_poll) hipHostFree(h_poll);
+    if (h_fault) hipHostFree(h_fault);
     hipFree(d_row_ptr); hipFree(d_col_idx); hipFree(d_col_idx_T); hipFree(d_col_ptr); hipFree(d_col_edge); hipFree(d_col_er); hipFree(d_row_pos);
     hipFree(d_unsat); hipFree(d_done); hipFree(d_fin); hipFree(d_fin_b); hipFree(d_fin_n);
     hipFree(d_sgn);
@@ -193,6 +194,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     if (res && !res_chosen && chunk > kResAutoMaxTiles * 64) res = false;
     nt_d = sched_flag(sched, LDPC_SCHED_NONTEMPORAL) && !res;  // the pool is meant to stay cached
     debug_no_drain = sched_flag(sched, LDPC_SCHED_DEBUG_NO_DRAIN);
+    debug_bad_lane = sched_flag(sched, LDPC_SCHED_DEBUG_BAD_LANE);
     var_cpw = sched.var_cpw;
     res_poll = sched.poll_every;
     if (chunk <= 0) {
@@ -259,6 +261,9 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
                                hipHostMallocCoherent | hipHostMallocMapped));
         std::memset(h_poll, 0, (size_t)kRing * sizeof(unsigned long long));
         LDPC_HIP(hipHostGetDevicePointer((void**)&d_poll, h_poll, 0));
+        LDPC_HIP(hipHostMalloc((void**)&h_fault, sizeof(unsigned long long), hipHostMallocCoherent | hipHostMallocMapped));
+        *h_fault = 0ull;
+        LDPC_HIP(hipHostGetDevicePointer((void**)&d_fault, h_fault, 0));
         LDPC_HIP(hipMalloc((void**)&d_unsat, (size_t)cap_tiles * sizeof(unsigned long long)));
         LDPC_HIP(hipMalloc((void**)&d_done, (size_t)cap_tiles * sizeof(unsigned int)));
         LDPC_HIP(hipMalloc((void**)&d_fin, (size_t)cap_tiles * sizeof(uint64_t)));
@@ -297,7 +302,7 @@ int32_t Engine::flags() const
     return (nt_d ? LDPC_SCHED_NONTEMPORAL : 0) | (cont ? LDPC_SCHED_CONTINUOUS : 0) |
            (msa_c ? LDPC_SCHED_MSA_COMPRESSED : 0) | (res ? LDPC_SCHED_RESIDENT : 0) |
            (syn_blocks > 0 ? LDPC_SCHED_SPLIT_SYNDROME : 0) | (first_fp ? LDPC_SCHED_FIRST_FROM_PRIOR : 0) |
-           (sched.flags & (LDPC_SCHED_LR_TABLE | LDPC_SCHED_DEBUG_NO_DRAIN));
+           (sched.flags & (LDPC_SCHED_LR_TABLE | LDPC_SCHED_DEBUG_NO_DRAIN | LDPC_SCHED_DEBUG_BAD_LANE));
 }
 
 // Placement probe.  The resident pool (~226 MB at 3 tiles) and the grouped
@@ -844,9 +849,10 @@ int Engine::poll_wait(uint64_t q, unsigned long long* occ)
         const unsigned long long v = *w;
         if ((v >> dev::kOccTileShift) == want) {
             *occ = v & dev::kOccMask;
-            return LDPC_OK;
+            return check_fault();
         }
         if (spin % 64 == 0) {
+            if (int rc = check_fault()) return rc;
             const hipError_t e = hipStreamQuery(stream);
             if (e == hipSuccess) {
                 const unsigned long long v2 = *w;
@@ -864,6 +870,34 @@ int Engine::poll_wait(uint64_t q, unsigned long long* occ)
             std::this_thread::yield();
         }
     }
+}
+
+int Engine::check_fault()
+{
+    if (!h_fault) return LDPC_OK;
+    volatile unsigned long long* w = h_fault;
+    const unsigned long long v = *w;
+    if (!(v & dev::kFaultTag)) return LDPC_OK;
+    *w = 0ull;
+    static const char* what[] = {"?", "iteration count / valid flag", "hard bits / posterior", "refill input row"};
+    const unsigned kind = (unsigned)((v >> 48) & 0x7fffu);
+    int64_t idx = (int64_t)(v & dev::kFaultIndex);
+    if (idx & (int64_t)(1ull << 47)) idx -= (int64_t)(1ull << 48);  // sign of the 48-bit field
+    if (kind == dev::kFaultSchedule)
+        set_error("device schedule fault: the code fill of tile " + std::to_string(-1 - idx) +
+                  " found live or finished lanes (skipped; the decode's outputs are incomplete)");
+    else
+        set_error(std::string("device lane bookkeeping fault: codeword index ") + std::to_string(idx) +
+                  " out of range for the " + (kind < 4 ? what[kind] : what[0]) +
+                  " access (skipped; the decode's outputs are incomplete)");
+    return LDPC_ERR_DEVICE;
+}
+
+int Engine::sync()
+{
+    LDPC_HIP(hipSetDevice(device));
+    LDPC_HIP(hipStreamSynchronize(stream));
+    return check_fault();
 }
 
 // Continuous batching over the whole batch: lanes are refilled as codewords
@@ -890,11 +924,15 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
                             stream, active, d_fresh, d_occ, d_ctr, 1 + kRing, d_unsat, d_done, tiles));
     ContState cs{active, d_fresh, d_occ, d_lane_b, d_lane_n, d_ctr, nullptr, B};
     cs.ntiles = tiles;
+    cs.fault = d_fault;
+    cs.debug_bad_lane = debug_bad_lane ? 1 : 0;
     const uint64_t q0 = poll_seq;  // this decode's first poll
     ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, ContOut{d_iters, d_valid}};
     const int hard_vec = ((uintptr_t)d_hard % 8 == 0 && N % 8 == 0) ? 1 : 0;
     Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
               d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
+    rf.nb = B;
+    rf.fault = d_fault;
     if (cur_codes) {  // coded input (decode_codes): int8 priors
         rf.in = nullptr;
         rf.in_code = cur_codes;
@@ -981,9 +1019,13 @@ int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_ite
         const int64_t gstep = low ? std::max(group_tiles, c2v_tiles) : group_tiles;
         if (ffp && cur_codes && s == 0 && N % 64 == 0) {
             // single fill on codes: step 0 is the transpose of the claimed
-            // rows into the lane codes (+ Init's decision ballots)
+            // rows into the lane codes (+ Init's decision ballots).  It stands
+            // in for that step's variable kernel because k_cont_reset left
+            // every lane empty, so step 0 has no live lane (active) and no
+            // finished one (fin) -- k_fill_codes checks both per tile and
+            // reports a violation as a device fault.
             LAUNCH(K_INIT, klaunch(k_fill_codes, dim3((unsigned)(N / 64), (unsigned)tiles), dim3(256), 0, stream,
-                                   cur_codes, d_lane_b, d_fresh, pcode, d_ptab, hard, N));
+                                   cur_codes, d_lane_b, d_fresh, pcode, d_ptab, hard, N, B, d_fault, active, d_fin));
             continue;  // (the poll of step 0 is never awaited)
         }
         for (int64_t t0 = 0; t0 < tiles; t0 += gstep) {

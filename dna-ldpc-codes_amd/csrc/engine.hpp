@@ -53,6 +53,7 @@ struct Engine {
     bool res = false;         // resident pool: a few tiles iterated in place, syndrome in the check kernel
     bool first_fp = false;    // single-fill BP: the first check reads the prior (k_check_bp_first)
     bool debug_no_drain = false;  // LDPC_SCHED_DEBUG_NO_DRAIN: the host ignores a drained pool
+    bool debug_bad_lane = false;  // LDPC_SCHED_DEBUG_BAD_LANE: one lane records an out-of-range codeword index
     int var_cpw = 4;          // variable phase: columns per wave (-2: by the prior's form, var_cpw_for)
     int res_poll = 8;         // res: steps between occupancy polls
     int syn_blocks = 0;       // continuous grouped mode: k_syndrome_split blocks per tile
@@ -77,6 +78,14 @@ struct Engine {
     unsigned long long* d_poll = nullptr;
     void poll_arm(dev::ContState& cs, uint64_t q) const;
     int poll_wait(uint64_t q, unsigned long long* occ);
+    // device fault word (kargs.hpp kFaultTag): pinned, device-mapped at d_fault
+    unsigned long long* h_fault = nullptr;
+    unsigned long long* d_fault = nullptr;
+    // LDPC_ERR_DEVICE (and the message) once a kernel has reported a fault;
+    // the word is cleared, so each fault is reported once
+    int check_fault();
+    // wait for the engine's stream, then check_fault
+    int sync();
     // graph on device
     int32_t* d_row_ptr = nullptr;
     int32_t* d_col_idx = nullptr;

@@ -33,6 +33,23 @@ struct Refill {
     const int8_t* in_code = nullptr;
     int8_t* pcode = nullptr;
     const double* ptab = nullptr;
+    // bounds of the lane codeword indices (fin_b, lane_b): the decode's B;
+    // a violation skips the access and is reported through `fault`
+    int64_t nb = 0;
+    unsigned long long* fault = nullptr;
+};
+
+// Device fault word (pinned host memory, device-mapped; ContState / Refill
+// ::fault): a kernel that finds a lane's codeword index outside [0, B)
+// skips the store or load it would address and writes kFaultTag | kind << 48
+// | (index & kFaultIndex); the host turns it into LDPC_ERR_DEVICE.
+constexpr unsigned long long kFaultTag = 1ull << 63;
+constexpr unsigned long long kFaultIndex = (1ull << 48) - 1ull;
+enum FaultKind : unsigned {
+    kFaultIters = 1,   // iteration count / valid flag of a finished codeword (cont_lanes)
+    kFaultOutput = 2,  // hard bits / posterior of a finished codeword (variable kernels)
+    kFaultRefill = 3,  // input row of a refilled lane (variable kernels, k_fill_codes)
+    kFaultSchedule = 4 // k_fill_codes on a tile with live or finished lanes (index: the tile)
 };
 
 // prior value of a code (coded input): table indexed by code + 128
@@ -58,6 +75,10 @@ struct ContState {
     unsigned long long* poll_host = nullptr;
     unsigned long long poll_tag = 0;
     int64_t ntiles = 0;
+    unsigned long long* fault = nullptr;  // see kFaultTag
+    // LDPC_SCHED_DEBUG_BAD_LANE (tests): the lane that claims codeword 0
+    // records the index B + 4096 instead, so the guarded accesses fire
+    int32_t debug_bad_lane = 0;
 };
 constexpr int kOccTileShift = 40;
 constexpr unsigned long long kOccMask = (1ull << kOccTileShift) - 1ull;

@@ -51,6 +51,20 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m)
     return ((uint64_t)hi << 32) | lo;
 }
 
+// A lane's codeword index b addresses the decode's outputs / input rows
+// only when 0 <= b < B.  Outside, the caller skips the access and the
+// fault word (kargs.hpp kFaultTag) records the kind and index for the host,
+// so broken lane bookkeeping ends as LDPC_ERR_DEVICE, not as an
+// out-of-bounds write.
+__device__ __forceinline__ bool lane_index_ok(int64_t b, int64_t B, unsigned long long* fault, unsigned kind)
+{
+    if (b >= 0 && b < B) return true;
+    if (fault)
+        __hip_atomic_store(fault, kFaultTag | ((unsigned long long)kind << 48) | ((unsigned long long)b & kFaultIndex),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return false;
+}
+
 // streaming access to the v2c ("d") array, optionally nontemporal
 template <bool NT>
 __device__ __forceinline__ double ld(const double* p)
@@ -142,7 +156,7 @@ __device__ __forceinline__ void cont_lanes(int64_t t, uint64_t occ, uint64_t U, 
         const bool fin = o && (!unsat || ln == max_iter);
         const bool cont = o && !fin;
         const int64_t b = o ? b0 : -1;
-        if (fin) { co.iters[b] = ln; co.valid[b] = unsat ? 0 : 1; }
+        if (fin && lane_index_ok(b, cs.B, cs.fault, kFaultIters)) { co.iters[b] = ln; co.valid[b] = unsat ? 0 : 1; }
         s_b[lane] = b;
         s_n[lane] = ln;
         const uint64_t F = __ballot(fin), Cm = __ballot(cont);
@@ -163,7 +177,12 @@ __device__ __forceinline__ void cont_lanes(int64_t t, uint64_t occ, uint64_t U, 
         const bool fresh = !cont && (base + (unsigned long long)rank < (unsigned long long)cs.B);
         const uint64_t Fr = __ballot(fresh);
         if (cont) cs.lane_n[li] = ln + 1;
-        if (fresh) { cs.lane_b[li] = (int64_t)(base + rank); cs.lane_n[li] = 0; }
+        if (fresh) {
+            int64_t nbv = (int64_t)(base + rank);
+            if (cs.debug_bad_lane && nbv == 0) nbv = cs.B + 4096;  // tests only (LDPC_SCHED_DEBUG_BAD_LANE)
+            cs.lane_b[li] = nbv;
+            cs.lane_n[li] = 0;
+        }
         if (lane == 0) {
             cs.active[t] = Cm;
             cs.fresh[t] = Fr;
@@ -518,20 +537,34 @@ __global__ __launch_bounds__(256, 2) void k_check_bp_first(const double* __restr
 // read as 64 contiguous bytes and each lane-code segment written as 64 --
 // instead of the variable kernel's per-lane byte gathers.  N % 64 == 0;
 // grid (N / 64, tiles), block 256.
+// It replaces the variable kernel of that step only because no lane of the
+// tile is live (active) or finished (fin) then: it neither updates nor
+// writes outputs.  A tile that breaks this is reported (kFaultSchedule) and
+// left alone.
 __global__ __launch_bounds__(256) void k_fill_codes(const int8_t* __restrict__ in_code,
                                                     const int64_t* __restrict__ lane_b,
                                                     const uint64_t* __restrict__ fresh, int8_t* __restrict__ pcode,
                                                     const double* __restrict__ ptab, uint64_t* __restrict__ hard,
-                                                    int32_t N)
+                                                    int32_t N, int64_t B, unsigned long long* fault,
+                                                    const uint64_t* __restrict__ active,
+                                                    const uint64_t* __restrict__ fin)
 {
     __shared__ int8_t sc[TILE][TILE + 4];
     __shared__ int64_t sb[TILE];
     const int64_t t = blockIdx.y;
     const uint64_t frm = fresh[t];
     if (frm == 0ull) return;  // block-uniform
+    if (active[t] != 0ull || fin[t] != 0ull) {  // block-uniform
+        if (threadIdx.x == 0) lane_index_ok(-1 - t, 0, fault, kFaultSchedule);
+        return;
+    }
     const int lane = lane_id(), w = wave_id();
     const int32_t j0 = (int32_t)blockIdx.x * TILE;
-    if (threadIdx.x < TILE) sb[lane] = ((frm >> lane) & 1ull) ? lane_b[t * TILE + lane] : -1;
+    if (threadIdx.x < TILE) {
+        int64_t b = ((frm >> lane) & 1ull) ? lane_b[t * TILE + lane] : -1;
+        if (b >= 0 && !lane_index_ok(b, B, fault, kFaultRefill)) b = -1;
+        sb[lane] = b;
+    }
     __syncthreads();
     for (int l = w; l < TILE; l += 4) {
         const int64_t b = sb[l];
@@ -639,13 +672,13 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
     if (touched == 0 && fm == 0) return;
     const bool live = (act >> lane) & 1ull;
     const bool fr = CONT && ((frm >> lane) & 1ull);
-    const bool fl = (fm >> lane) & 1ull;
     int64_t fb = 0;
     int32_t fn = 0;
-    if (fl) {
+    if ((fm >> lane) & 1ull) {
         fb = rf.fin_b[t * TILE + lane];
         fn = rf.fin_n[t * TILE + lane];
     }
+    const bool fl = ((fm >> lane) & 1ull) && lane_index_ok(fb, rf.nb, rf.fault, kFaultOutput);
     const size_t tb = (size_t)t * E;
     int32_t eid[CPW][DV];
 #pragma unroll
@@ -655,7 +688,9 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
     double l[CPW][DV], pv[CPW], xin[CPW];
     int8_t kin[CPW];  // PC: the refilled lane's input codes
     if (fr) {  // refilled lane: its input row, prefetched with the c2v loads
-        const size_t rb = (size_t)rf.lane_b[t * TILE + lane] * N;
+        int64_t b = rf.lane_b[t * TILE + lane];
+        if (!lane_index_ok(b, rf.nb, rf.fault, kFaultRefill)) b = 0;
+        const size_t rb = (size_t)b * N;
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             if constexpr (PC) kin[c] = rf.in_code[rb + j0 + c];
@@ -1163,13 +1198,13 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
     if (touched == 0 && fm == 0) return;
     const bool live = (act >> lane) & 1ull;
     const bool fr = CONT && ((frm >> lane) & 1ull);
-    const bool fl = (fm >> lane) & 1ull;
     int64_t fb = 0;
     int32_t fn = 0;
-    if (fl) {
+    if ((fm >> lane) & 1ull) {
         fb = rf.fin_b[t * TILE + lane];
         fn = rf.fin_n[t * TILE + lane];
     }
+    const bool fl = ((fm >> lane) & 1ull) && lane_index_ok(fb, rf.nb, rf.fault, kFaultOutput);
     uint32_t er[CPW][DV];
 #pragma unroll
     for (int c = 0; c < CPW; ++c)
@@ -1182,7 +1217,9 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
     double l[CPW][DV], pv[CPW], xin[CPW];
     int8_t kin[CPW];  // PC: the refilled lane's input codes
     if (fr) {
-        const size_t rb = (size_t)rf.lane_b[t * TILE + lane] * N;
+        int64_t b = rf.lane_b[t * TILE + lane];
+        if (!lane_index_ok(b, rf.nb, rf.fault, kFaultRefill)) b = 0;
+        const size_t rb = (size_t)b * N;
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             if constexpr (PC) kin[c] = rf.in_code[rb + j0 + c];

@@ -29,7 +29,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libldpc_amd.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 LDPC_OK, LDPC_ERR_ARG, LDPC_ERR_IO, LDPC_ERR_FORMAT, LDPC_ERR_DEVICE, LDPC_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
 
 
@@ -77,7 +77,7 @@ class LdpcError(RuntimeError):
 # ldpc_schedule flag bits (include/ldpc_amd.h LDPC_SCHED_*) by keyword
 SCHED_FLAGS = {"nontemporal": 1 << 0, "continuous": 1 << 3, "msa_compressed": 1 << 4, "resident": 1 << 5,
                "split_syndrome": 1 << 6, "first_from_prior": 1 << 12, "lr_table": 1 << 13,
-               "debug_no_drain": 1 << 14}
+               "debug_no_drain": 1 << 14, "debug_bad_lane": 1 << 15}
 SCHED_FIELDS = ("group_tiles", "var_cpw", "pool_tiles", "poll_every", "syn_blocks")
 
 
@@ -149,9 +149,12 @@ def lib():
             raise ImportError(f"{LIB_PATH} is missing: build it with `make -C dna-ldpc-codes_amd` "
                               "(there is no CPU fallback)")
         L = C.CDLL(LIB_PATH)
-        if L.ldpc_abi_version() != ABI_VERSION:
-            raise ImportError(f"{LIB_PATH}: ABI version {L.ldpc_abi_version()}, this shim needs {ABI_VERSION} "
-                              "(rebuild with `make -C dna-ldpc-codes_amd`)")
+        missing = [n for n in EXPORTS if not hasattr(L, n)]
+        version = L.ldpc_abi_version() if "ldpc_abi_version" not in missing else None
+        if missing or version != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH}: ABI version {version}, this shim needs {ABI_VERSION}"
+                              + (f"; missing symbols {missing}" if missing else "")
+                              + " (rebuild with `make -C dna-ldpc-codes_amd`)")
         vp, i32, i64, dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_double
         pint = C.POINTER(C.c_int)
         L.ldpc_abi_version.restype = C.c_int

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LDPC_AMD_ABI_VERSION 2
+#define LDPC_AMD_ABI_VERSION 3
 
 /* error codes */
 enum {
@@ -98,8 +98,12 @@ enum {
                                            lattice cross PCIe as one byte each and are decoded as codes with the
                                            table k * unit (BP: its host exp), as ldpc_engine_decode_codes
                                            (default on; off = fp64 input: host exp / copy of every value) */
-    LDPC_SCHED_DEBUG_NO_DRAIN = 1 << 14 /* tests only: the host ignores a drained pool, so a decode runs
+    LDPC_SCHED_DEBUG_NO_DRAIN = 1 << 14, /* tests only: the host ignores a drained pool, so a decode runs
                                            into its step bound and returns LDPC_ERR_DEVICE (default off) */
+    LDPC_SCHED_DEBUG_BAD_LANE = 1 << 15 /* tests only (continuous schedules): the lane that claims codeword 0
+                                           records an out-of-range index instead; the kernels' bounds checks
+                                           skip its output stores and input reads and the decode returns
+                                           LDPC_ERR_DEVICE (default off) */
 };
 
 typedef struct ldpc_schedule {

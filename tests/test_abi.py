@@ -27,7 +27,19 @@ def test_exports_match_header(L):
     lib = L.lib()
     for name in declared:
         assert hasattr(lib, name)
-    assert lib.ldpc_abi_version() == 2 == L.ABI_VERSION
+    assert lib.ldpc_abi_version() == 3 == L.ABI_VERSION
+
+
+def test_stale_library_is_a_clear_import_error(L, monkeypatch):
+    """A library that lacks a symbol the shim binds (a stale build) fails
+    lib() with the ABI ImportError, not an AttributeError while binding."""
+    L.lib()
+    monkeypatch.setattr(L, "EXPORTS", L.EXPORTS + ["ldpc_not_in_this_build"])
+    monkeypatch.setattr(L, "_lib", None)
+    with pytest.raises(ImportError, match="missing symbols .*ldpc_not_in_this_build"):
+        L.lib()
+    monkeypatch.undo()
+    assert L.lib() is not None
 
 
 def test_graph_load_matches_oracle(L, og):

@@ -53,7 +53,7 @@ def test_roofline_moved_bytes():
     assert rm["moved_bytes_per_cw_iter"] == rm["algorithmic_bytes_per_cw_iter"] - 7 * G.N
     assert abs(rm["achieved_moved"] / rm["achieved"] - rm["moved_bytes_per_cw_iter"] /
                rm["algorithmic_bytes_per_cw_iter"]) < 1e-3
-    assert rm["frac_of_measured_ceiling"] == round(rm["achieved_moved"] / rm["ceiling_measured"], 4)
+    assert rm["frac_moved_of_measured_ceiling"] == round(rm["achieved_moved"] / rm["ceiling_measured"], 4)
     rf = b.roofline(_eng(msa_compressed=True, resident=False, nontemporal=True, algo=1), G, st, cw_iters, coded=False)
     assert rf["achieved_moved"] == rf["achieved"]
 
@@ -82,3 +82,14 @@ def test_kernel_names_match_the_committed_trace_and_traffic_table():
         for kind, name in names.items():
             assert name in traced, (kind, name)
             assert name in known, (kind, name)
+
+
+def test_config4_leg_selection():
+    """BASELINE config 4 (1M codewords over 8 GPUs) runs inside the driver's
+    8-GPU weak-scaling bench by default; --config4 G forces it at N > 1."""
+    b = _bench()
+    assert b.config4_total("auto", 8, 0) == 1_000_000
+    assert b.config4_total("auto", 8, 1_000_000) == 0  # the headline already is config 4
+    assert [b.config4_total("auto", n, 0) for n in (1, 2, 4)] == [0, 0, 0]
+    assert b.config4_total("4096", 2, 0) == 4096 and b.config4_total("4096", 1, 0) == 0
+    assert b.config4_total("0", 8, 0) == 0

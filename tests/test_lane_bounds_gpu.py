@@ -1,0 +1,92 @@
+"""Every store (and input read) a kernel addresses through a lane's codeword
+index is bounds-checked (kernels.hpp lane_index_ok): the finished codeword's
+iteration count / valid flag (cont_lanes), its hard bits and posterior
+(k_var_m / k_var_msa_c), and a refilled lane's input row (the variable
+kernels, k_fill_codes).  An index outside [0, B) skips the access and writes
+the engine's fault word; the host reports LDPC_ERR_DEVICE with the index.
+
+The LDPC_SCHED_DEBUG_BAD_LANE schedule bit stands in for broken lane
+bookkeeping (round 4's illegal-address fault came from a stale lane index):
+the lane that claims codeword 0 records B + 4096 instead.  Each continuous
+schedule must end in LDPC_ERR_DEVICE naming that index -- never in a device
+fault -- and the next clean decode on the same graph equals the oracle."""
+import numpy as np
+import pytest
+
+import synth
+from conftest import PCHK
+from test_gpu_parity import _cmp
+
+pytestmark = pytest.mark.gpu
+
+SCHEDULES = [
+    ("bp", {}),                          # resident pool (check kernel's bookkeeping, k_var_m in place)
+    ("bp", {"resident": False}),         # grouped: k_syndrome_split + k_var_m
+    ("msa", {}),                         # compressed min-sum: k_var_msa_c
+    ("msa", {"msa_compressed": False}),  # fp64 min-sum, resident pool
+]
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("algo,sch", SCHEDULES)
+def test_bad_lane_index_is_reported_not_written(gpu, og, codewords, algo, sch):
+    L = gpu
+    G2 = L.Graph(PCHK)
+    B = 150
+    llr = synth.bsc_llrs(codewords, 0, B, seed=5, p=0.003)
+    with pytest.raises(L.LdpcError) as e:
+        G2.decode(llr, max_iter=6, algo=algo, post="llr", schedule=dict(sch, debug_bad_lane=True))
+    assert e.value.code == L.LDPC_ERR_DEVICE, str(e.value)
+    assert "out of range" in str(e.value) and str(B + 4096) in str(e.value), str(e.value)
+    _cmp(G2, og, llr, 6, algo=algo, schedule=sch)
+
+
+@pytest.mark.timeout(120)
+def test_bad_lane_index_single_fill_codes(gpu, og, codewords):
+    """The DNA batch's path: one fill of the lane pool from int8 codes, whose
+    step 0 is k_fill_codes' transpose of the claimed rows."""
+    L = gpu
+    G2 = L.Graph(PCHK)
+    llr = synth.dna_like_llrs(codewords, seed=1)  # 272 codewords: one grouped fill of 5 tiles
+    k = np.rint(llr / synth.LLR_UNIT).astype(np.int8)
+    assert np.array_equal(k * synth.LLR_UNIT, llr)
+    table = np.arange(-128, 128, dtype=np.float64) * synth.LLR_UNIT
+    with pytest.raises(L.LdpcError) as e:
+        G2.decode_codes(k, table, max_iter=20, post=None, schedule={"debug_bad_lane": True})
+    assert e.value.code == L.LDPC_ERR_DEVICE and "out of range" in str(e.value), str(e.value)
+    h, _, it, v = G2.decode_codes(k, table, max_iter=20, post=None)
+    rh, _, rit, rv = og.decode_batch(llr, 20, threads=8, want_post=False)
+    assert np.array_equal(h, rh) and np.array_equal(it, rit) and np.array_equal(v, rv.astype(bool))
+
+
+@pytest.mark.timeout(120)
+def test_bad_lane_index_engine_api(gpu, codewords):
+    """Through the device-resident engine: the fault surfaces at the next
+    occupancy poll or at ldpc_engine_sync, and the engine decodes cleanly
+    afterwards."""
+    L = gpu
+    G2 = L.Graph(PCHK)
+    B, N = 300, G2.N
+    llr = synth.bsc_llrs(codewords, 0, B, seed=6, p=0.003)
+    d_in = L.DeviceBuffer(0, B * N * 8)
+    d_in.upload(np.ascontiguousarray(llr))
+    d_h, d_i, d_v = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
+    bad = L.Engine(G2, 0, "bp", debug_bad_lane=True)
+    with pytest.raises(L.LdpcError) as e:
+        bad.decode(d_in.at(0), L.IN_LLR, B, 6, d_h.at(0), None, L.POST_LLR, d_i.at(0), d_v.at(0))
+        bad.sync()
+    assert e.value.code == L.LDPC_ERR_DEVICE and str(B + 4096) in str(e.value), str(e.value)
+    try:  # steps enqueued before the report may flag the lane again
+        bad.sync()
+    except L.LdpcError:
+        pass
+    bad.close()
+    ok = L.Engine(G2, 0, "bp")
+    ok.decode(d_in.at(0), L.IN_LLR, B, 6, d_h.at(0), None, L.POST_LLR, d_i.at(0), d_v.at(0))
+    ok.sync()
+    h, _, it, v = G2.decode(llr, max_iter=6, post=None)
+    assert np.array_equal(d_h.download(np.empty((B, N), np.uint8)), h)
+    assert np.array_equal(d_i.download(np.empty(B, np.int32)), it)
+    ok.close()
+    for b in (d_in, d_h, d_i, d_v):
+        b.free()

@@ -113,6 +113,31 @@ def test_plain_bench_gpus2_runs_two_ranks(gpu, single_process_dump, tmp_path):
     _check_two_rank_run(r.stdout, d2, single_process_dump)
 
 
+@pytest.mark.timeout(300)
+def test_plain_bench_gpus2_cpu_baseline_and_config4_leg(gpu):
+    """The N > 1 line carries what the driver's 8-GPU run needs by itself:
+    rank 0's cpu_baseline (the oracle timed on the host cores while rank 1
+    waits) and the config-4 leg -- here forced at a 1000-codeword global
+    batch -- with both ranks' oracle checks of their dist.shard ranges."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch-per-gpu", "256",
+                        "--max-iter", "20", "--p", "0.0065", "--steps", "1", "--warmup", "0", "--no-profile",
+                        "--cpu-seconds", "1", "--config4", "1000"], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _line(r.stdout)
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak" and out["check"]["mismatches"] == 0
+    cb = out["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["checked"] > 0
+    assert cb["mismatches"] == 0 and "barrier" in cb["while"]
+    leg = out["secondary"]["config4_strong"]
+    assert leg["global_batch"] == 1000 and leg["per_rank"] == [500, 500] and leg["scaling"] == "strong"
+    assert leg["value"] > 0 and leg["check"]["mismatches"] == 0
+    per = leg["check"]["per_rank"]
+    assert [p["rank"] for p in per] == [0, 1] and [p["b0"] for p in per] == [0, 500]
+    for p in per:
+        assert p["checked"] >= 16 and p["rows"]["tail"][1] == 500 and len(p["rows"]["interior"]) > 0
+
+
 def test_bench_global_batch_odd_split(gpu, tmp_path):
     """A global batch that does not divide: dist.shard sizes differ by one;
     single process -> the whole range."""
