@@ -261,8 +261,9 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
                                hipHostMallocCoherent | hipHostMallocMapped));
         std::memset(h_poll, 0, (size_t)kRing * sizeof(unsigned long long));
         LDPC_HIP(hipHostGetDevicePointer((void**)&d_poll, h_poll, 0));
-        LDPC_HIP(hipHostMalloc((void**)&h_fault, sizeof(unsigned long long), hipHostMallocCoherent | hipHostMallocMapped));
-        *h_fault = 0ull;
+        LDPC_HIP(hipHostMalloc((void**)&h_fault, dev::kFaultWords * sizeof(unsigned long long),
+                               hipHostMallocCoherent | hipHostMallocMapped));
+        std::memset(h_fault, 0, dev::kFaultWords * sizeof(unsigned long long));
         LDPC_HIP(hipHostGetDevicePointer((void**)&d_fault, h_fault, 0));
         LDPC_HIP(hipMalloc((void**)&d_unsat, (size_t)cap_tiles * sizeof(unsigned long long)));
         LDPC_HIP(hipMalloc((void**)&d_done, (size_t)cap_tiles * sizeof(unsigned int)));
@@ -876,20 +877,27 @@ int Engine::check_fault()
 {
     if (!h_fault) return LDPC_OK;
     volatile unsigned long long* w = h_fault;
-    const unsigned long long v = *w;
-    if (!(v & dev::kFaultTag)) return LDPC_OK;
-    *w = 0ull;
-    static const char* what[] = {"?", "iteration count / valid flag", "hard bits / posterior", "refill input row"};
-    const unsigned kind = (unsigned)((v >> 48) & 0x7fffu);
-    int64_t idx = (int64_t)(v & dev::kFaultIndex);
-    if (idx & (int64_t)(1ull << 47)) idx -= (int64_t)(1ull << 48);  // sign of the 48-bit field
-    if (kind == dev::kFaultSchedule)
-        set_error("device schedule fault: the code fill of tile " + std::to_string(-1 - idx) +
-                  " found live or finished lanes (skipped; the decode's outputs are incomplete)");
-    else
-        set_error(std::string("device lane bookkeeping fault: codeword index ") + std::to_string(idx) +
-                  " out of range for the " + (kind < 4 ? what[kind] : what[0]) +
-                  " access (skipped; the decode's outputs are incomplete)");
+    std::string msg;
+    for (int k = 1; k < dev::kFaultWords; k++) {  // every word is read and cleared; the first set one is reported
+        const unsigned long long v = w[k];
+        if (!(v & dev::kFaultTag)) continue;
+        w[k] = 0ull;
+        if (!msg.empty()) continue;
+        int64_t idx = (int64_t)(v & dev::kFaultIndex);
+        if (idx & (int64_t)(1ull << 47)) idx -= (int64_t)(1ull << 48);  // sign of the 48-bit field
+        if (k == dev::kFaultSchedule)
+            msg = "device schedule fault: the code fill of tile " + std::to_string(-1 - idx) +
+                  " found live or finished lanes";
+        else if (k == dev::kFaultOutput)
+            msg = "device lane bookkeeping fault: the finished codeword of pool slot " + std::to_string(idx) +
+                  " has a codeword index out of range for its hard bits / posterior";
+        else
+            msg = std::string("device lane bookkeeping fault: codeword index ") + std::to_string(idx) +
+                  " out of range for the " + (k == dev::kFaultIters ? "iteration count / valid flag" : "refill input row") +
+                  " access";
+    }
+    if (msg.empty()) return LDPC_OK;
+    set_error(msg + " (skipped; the decode's outputs are incomplete)");
     return LDPC_ERR_DEVICE;
 }
 

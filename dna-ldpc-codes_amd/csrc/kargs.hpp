@@ -39,18 +39,20 @@ struct Refill {
     unsigned long long* fault = nullptr;
 };
 
-// Device fault word (pinned host memory, device-mapped; ContState / Refill
-// ::fault): a kernel that finds a lane's codeword index outside [0, B)
-// skips the store or load it would address and writes kFaultTag | kind << 48
-// | (index & kFaultIndex); the host turns it into LDPC_ERR_DEVICE.
+// Device fault words (pinned host memory, device-mapped; ContState / Refill
+// ::fault, one word per FaultKind): a kernel that finds a lane's codeword
+// index outside [0, B) skips the store or load it would address and writes
+// kFaultTag | kind << 48 | (index & kFaultIndex) to fault[kind]; the host
+// turns the first nonzero word into LDPC_ERR_DEVICE.
 constexpr unsigned long long kFaultTag = 1ull << 63;
 constexpr unsigned long long kFaultIndex = (1ull << 48) - 1ull;
 enum FaultKind : unsigned {
     kFaultIters = 1,   // iteration count / valid flag of a finished codeword (cont_lanes)
-    kFaultOutput = 2,  // hard bits / posterior of a finished codeword (variable kernels)
+    kFaultOutput = 2,  // hard bits / posterior of a finished codeword (variable kernels; index: the lane's pool slot)
     kFaultRefill = 3,  // input row of a refilled lane (variable kernels, k_fill_codes)
     kFaultSchedule = 4 // k_fill_codes on a tile with live or finished lanes (index: the tile)
 };
+constexpr int kFaultWords = 5;  // fault[0] unused
 
 // prior value of a code (coded input): table indexed by code + 128
 constexpr int kCodeBias = 128;
