@@ -33,10 +33,13 @@ bits, iteration counts and valid flags must equal the GPU's; `check` in the
 JSON line carries the per-rank counts and rows, and any mismatch exits
 non-zero.
 
-At N = 1 (unless --secondary 0) two driver-timed secondary legs follow the
-headline, each with its own oracle check, under "secondary": config 2 (the
-272-codeword DNA batch through the host API ldpc_decode, median of 15 calls)
-and config 5 (1M codewords, min-sum with early exit, 2 timed steps).
+At N = 1 (unless --secondary 0) driver-timed secondary legs follow the
+headline, each with its own oracle check, under "secondary": the headline on
+fp64 input, the headline's kernels streaming from HBM (16384 codewords in one
+pass, 38.7 GB of messages: the HBM-only roofline beside the headline's
+Infinity-Cache-resident pool), config 2 (the 272-codeword DNA batch through
+the host API ldpc_decode, median of 15 calls) and config 5 (1M codewords,
+min-sum with early exit, 2 timed steps).
 
 At N > 1, after the headline and every rank's check: rank 0 times the oracle
 on all the host cores it may use while the other ranks wait in a barrier
@@ -103,6 +106,8 @@ def parse():
     ap.add_argument("--secondary", type=int, default=1,
                     help="N = 1: also time config 2 (DNA batch, host API) and config 5 (1M min-sum) after the headline")
     ap.add_argument("--msa-batch", type=int, default=1_000_000, help="config-5 secondary leg: codewords")
+    ap.add_argument("--hbm-batch", type=int, default=16384,
+                    help="HBM-streaming secondary leg: codewords in its one pass (0: skip the leg)")
     ap.add_argument("--input", default="code", choices=["code", "fp64"],
                     help="channel output in HBM: int8 codes + a 256-entry table (default) or fp64 LR / LLR")
     ap.add_argument("--workload", default="bsc", choices=["bsc", "dna272"],
@@ -277,6 +282,9 @@ def _bound_detail(eng) -> str:
                 "fabric interface once per phase (PMC fabric bytes = 1.02-1.04 x algorithmic), served by HBM and the "
                 "Infinity Cache; the DRAM-request counters count cache hits too on gfx950 (calibrated), so the cache "
                 "share is not observable; no MFMA")
+    if eng.group_tiles * 64 * 147456 * 8 > 256 * 2 ** 20:
+        return ("one grouped pass over every tile: the c2v scratch and the v2c stream (nontemporal) both exceed the "
+                "256 MB Infinity Cache, so every message byte streams from HBM; memory-bound, no MFMA")
     return ("grouped schedule: the group's c2v scratch is meant to stay in the Infinity Cache between the phases, the "
             "v2c stream goes to HBM (nontemporal); memory-bound, no MFMA")
 
@@ -521,6 +529,64 @@ def fp64_leg(args, L, eng, G, dev, b0, B, d_cw, n_cw, in_kind, iters, valid, d_h
             "same_as_coded": same, "compared": f"iterations + valid flags of all {B}, hard bits of {len(rows)} codewords",
             "check": {"checked": len(rows), "mismatches": 0 if same else 1,
                       "what": "the fp64-input decode vs the coded headline decode (bit-identical)"}}
+
+
+def hbm_stream(args, og, threads, cw, d_cw, B=16384):
+    """The headline's kernels with nothing resident in a cache: BP on
+    `B` codewords of the config-3 channel in ONE grouped pass (no resident
+    pool, the check / variable launches span every tile, v2c and c2v
+    2 x B x 1.18 MB = 38.7 GB at B = 16384, far beyond the 256 MB Infinity
+    Cache), 1 warm-up + 2 timed decodes.  Its roofline is the HBM-streaming
+    rate of the same arithmetic, beside the headline's Infinity-Cache-resident
+    pool; 16 codewords (both ends) oracle-checked."""
+    import ldpc_amd as L
+    import synth
+    G = L.Graph(synth.PCHK)
+    N = G.N
+    eng = L.Engine(G, 0, "bp", chunk=B, resident=False, group_tiles=-1)
+    d_in, decode = channel(L, eng, args, 0, N, 0, B, d_cw, cw.shape[0], args.p, L.IN_LR)
+    d_hard, d_iters, d_valid = L.DeviceBuffer(0, B * N), L.DeviceBuffer(0, B * 4), L.DeviceBuffer(0, B)
+
+    def step():
+        decode(B, args.max_iter, d_hard.at(0), d_iters.at(0), d_valid.at(0))
+
+    step()
+    eng.sync()
+    eng.profile(0 if args.no_profile else 4)
+    steps = 2
+    t = time.perf_counter()
+    for _ in range(steps):
+        step()
+    eng.sync()
+    el = time.perf_counter() - t
+    st = eng.stats()
+    iters = d_iters.download(np.empty(B, np.int32))
+    valid = d_valid.download(np.empty(B, np.uint8))
+    cw_iters = float(iters.sum()) * steps
+    rl = roofline(eng, G, st, cw_iters, args.input == "code")
+    out = {"workload": f"bsc-p{args.p}-{B // 1000}k-bp{args.max_iter}-one-pass", "batch": B, "steps": steps,
+           "value": round(B * steps / el, 1), "unit": "codewords/s", "ms_per_step": round(el / steps * 1e3, 2),
+           "schedule": {"resident_pool": eng.resident, "group_tiles": eng.group_tiles, "tiles": -(-B // 64),
+                        "nontemporal_d": eng.nontemporal},
+           "working_set_GB": round(2 * B * G.E * 8 / 1e9, 1),
+           "roofline": rl,
+           "note": "diagnostic: every message byte streams from HBM (working set >> 256 MB); the headline's pool "
+                   "stays in the Infinity Cache, so its `frac` is of bytes through L2 -> fabric, served by both"}
+    if og is not None:
+        def llr_fn(start, k):
+            return synth.bsc_llrs(cw, start, k, seed=args.seed, p=args.p)
+
+        def gpu_out(start, k):
+            h = d_hard.download(np.empty((k, N), np.uint8), offset=start * N)
+            return h, iters[start:start + k], valid[start:start + k]
+
+        checked, bad, _ = oracle_check(og, llr_fn, gpu_out, 0, args.max_iter, [(0, 8), (B - 8, 8)], threads)
+        out["check"] = {"checked": checked, "mismatches": len(bad), "first_mismatches": bad[:8],
+                        "what": "first and last 8 codewords of the timed decode vs the oracle"}
+    for b in (d_in, d_hard, d_iters, d_valid):
+        b.free()
+    eng.close()
+    return out
 
 
 def msa_1m(args, og, threads, cw, d_cw):
@@ -844,7 +910,7 @@ def main():
                             "config4_1m_strong" if c4 == 1_000_000 else "config4_strong": leg}
         mismatches += leg["check"]["mismatches"]
 
-    # ---- secondary legs (N = 1): config 3 on fp64 input, config 5 and config 2, each checked ----
+    # ---- secondary legs (N = 1): config 3 on fp64 input and streaming from HBM, config 5, config 2; each checked ----
     if world == 1 and args.secondary and args.global_batch == 0 and algo == "bp":
         sec = {"note": "driver-timed after the headline region; not part of value / ms_per_step"}
         if args.input == "code":
@@ -855,6 +921,10 @@ def main():
         for b in (d_in, d_hard, d_iters, d_valid):
             b.free()
         eng.close()
+        if args.hbm_batch > 0:
+            t = time.perf_counter()
+            sec["config3_hbm_streaming"] = hbm_stream(args, og, cpus["effective"], cw, d_cw, B=args.hbm_batch)
+            sec["config3_hbm_streaming"]["leg_wall_s"] = round(time.perf_counter() - t, 2)
         t = time.perf_counter()
         sec["config5_msa_1m"] = msa_1m(args, og, cpus["effective"], cw, d_cw)
         sec["config5_msa_1m"]["leg_wall_s"] = round(time.perf_counter() - t, 2)

@@ -888,13 +888,12 @@ int Engine::check_fault()
         if (k == dev::kFaultSchedule)
             msg = "device schedule fault: the code fill of tile " + std::to_string(-1 - idx) +
                   " found live or finished lanes";
-        else if (k == dev::kFaultOutput)
-            msg = "device lane bookkeeping fault: the finished codeword of pool slot " + std::to_string(idx) +
-                  " has a codeword index out of range for its hard bits / posterior";
-        else
-            msg = std::string("device lane bookkeeping fault: codeword index ") + std::to_string(idx) +
-                  " out of range for the " + (k == dev::kFaultIters ? "iteration count / valid flag" : "refill input row") +
-                  " access";
+        else if (k == dev::kFaultIters)
+            msg = "device lane bookkeeping fault: codeword index " + std::to_string(idx) +
+                  " out of range for the iteration count / valid flag access";
+        else  // the variable kernels report the lane's pool slot (k_fill_codes the codeword index)
+            msg = "device lane bookkeeping fault: pool slot or codeword index " + std::to_string(idx) +
+                  " out of range for " + (k == dev::kFaultOutput ? "a finished codeword's hard bits / posterior" : "a refill's input row");
     }
     if (msg.empty()) return LDPC_OK;
     set_error(msg + " (skipped; the decode's outputs are incomplete)");

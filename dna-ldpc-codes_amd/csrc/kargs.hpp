@@ -49,7 +49,7 @@ constexpr unsigned long long kFaultIndex = (1ull << 48) - 1ull;
 enum FaultKind : unsigned {
     kFaultIters = 1,   // iteration count / valid flag of a finished codeword (cont_lanes)
     kFaultOutput = 2,  // hard bits / posterior of a finished codeword (variable kernels; index: the lane's pool slot)
-    kFaultRefill = 3,  // input row of a refilled lane (variable kernels, k_fill_codes)
+    kFaultRefill = 3,  // input row of a refilled lane (variable kernels: index = the lane's pool slot; k_fill_codes)
     kFaultSchedule = 4 // k_fill_codes on a tile with live or finished lanes (index: the tile)
 };
 constexpr int kFaultWords = 5;  // fault[0] unused

@@ -68,13 +68,24 @@ __device__ __forceinline__ void lane_fault(unsigned long long* fault, unsigned k
 // out-of-bounds write.
 __device__ __forceinline__ bool lane_index_ok(int64_t b, int64_t B, unsigned long long* fault, unsigned kind)
 {
-#ifdef LDPC_AB_NO_LANE_GUARD  // same-box A/B of the guards' cost only (tools/build_ab.sh)
-    return true;
-#endif
     if (b >= 0 && b < B) return true;
     lane_fault(fault, kind, b);
     return false;
 }
+
+// The variable kernels' two lane-indexed accesses, checked by plain compares
+// whose faults are reported at the end of the kernel (lane_fault, by the
+// lane's pool slot): a report branch between a refilled lane's lane_b load
+// and its input-row load cost config 5 2 % (profiles/r5/README.md).
+//   refill_row: a refilled lane's input row, row 0 when b is out of range
+//   out_ok:     the finished codeword's index bounds at its output stores
+__device__ __forceinline__ int64_t refill_row(int64_t b, const Refill& rf, bool& bad)
+{
+    const bool ok = (uint64_t)b < (uint64_t)rf.nb;
+    bad = !ok;
+    return ok ? b : 0;
+}
+__device__ __forceinline__ bool out_ok(int64_t fb, const Refill& rf) { return (uint64_t)fb < (uint64_t)rf.nb; }
 
 // streaming access to the v2c ("d") array, optionally nontemporal
 template <bool NT>
@@ -698,10 +709,9 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
         for (int s = 0; s < DV; ++s) eid[c][s] = col_edge[(size_t)(j0 + c) * DV + s];
     double l[CPW][DV], pv[CPW], xin[CPW];
     int8_t kin[CPW];  // PC: the refilled lane's input codes
+    bool bad_in = false;  // a refilled lane's out-of-range index (reported at the end)
     if (fr) {  // refilled lane: its input row, prefetched with the c2v loads
-        int64_t b = rf.lane_b[t * TILE + lane];
-        if (!lane_index_ok(b, rf.nb, rf.fault, kFaultRefill)) b = 0;
-        const size_t rb = (size_t)b * N;
+        const size_t rb = (size_t)refill_row(rf.lane_b[t * TILE + lane], rf, bad_in) * N;
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             if constexpr (PC) kin[c] = rf.in_code[rb + j0 + c];
@@ -726,7 +736,7 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
     // (a check with its fault report where fin_b is loaded makes every wave
     // wait for that load before its message loads: config 5 -2.4 %); the
     // report itself comes last (lane_fault_report)
-    const bool fok = (uint64_t)fb < (uint64_t)rf.nb;
+    const bool fok = out_ok(fb, rf);
     if (CONT && fl && fok) {  // finished codeword: hard bits of its exit (ballots before this step's update)
         uint64_t hw[CPW];
 #pragma unroll
@@ -820,9 +830,10 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
             hard[o] = (old & ~touched) | (m & touched);
         }
     }
-    // the skipped stores' report: the lane's pool slot (fb need not stay live;
-    // cont_lanes reports the index itself when it is out of range there)
+    // the reports of skipped accesses: the lane's pool slot (the indices need
+    // not stay live; cont_lanes reports an out-of-range index itself)
     if (CONT && fl && !fok) lane_fault(rf.fault, kFaultOutput, t * TILE + lane);
+    if (bad_in) lane_fault(rf.fault, kFaultRefill, t * TILE + lane);
 }
 
 template <bool MSA, int DV, bool NT, bool CONT, int CPW, bool INPLACE, bool PC = false>
@@ -1235,10 +1246,9 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
     static_assert(CONT || !PC, "coded priors come with continuous refills");
     double l[CPW][DV], pv[CPW], xin[CPW];
     int8_t kin[CPW];  // PC: the refilled lane's input codes
+    bool bad_in = false;  // as k_var_m
     if (fr) {
-        int64_t b = rf.lane_b[t * TILE + lane];
-        if (!lane_index_ok(b, rf.nb, rf.fault, kFaultRefill)) b = 0;
-        const size_t rb = (size_t)b * N;
+        const size_t rb = (size_t)refill_row(rf.lane_b[t * TILE + lane], rf, bad_in) * N;
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             if constexpr (PC) kin[c] = rf.in_code[rb + j0 + c];
@@ -1313,7 +1323,7 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
 #pragma unroll
             for (int s = 0; s < DV; ++s) l[c][s] = flip_sign(l[c][s], cpk[c] >> (4 * s));
     }
-    const bool fok = (uint64_t)fb < (uint64_t)rf.nb;  // index bounds, as k_var_m
+    const bool fok = out_ok(fb, rf);  // index bounds, as k_var_m
     if (CONT && fl && fok) {  // finished codeword: hard bits of its exit (ballots before this step's update)
         uint64_t hw[CPW];
 #pragma unroll
@@ -1377,9 +1387,10 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
             hard[o] = (old & ~touched) | (m & touched);
         }
     }
-    // the skipped stores' report: the lane's pool slot (fb need not stay live;
-    // cont_lanes reports the index itself when it is out of range there)
+    // the reports of skipped accesses: the lane's pool slot (the indices need
+    // not stay live; cont_lanes reports an out-of-range index itself)
     if (CONT && fl && !fok) lane_fault(rf.fault, kFaultOutput, t * TILE + lane);
+    if (bad_in) lane_fault(rf.fault, kFaultRefill, t * TILE + lane);
 }
 
 // ---------------------------------------------------------------------------

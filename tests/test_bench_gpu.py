@@ -46,7 +46,7 @@ def test_bench_secondary_legs(gpu):
     """The driver-run line's secondary legs (config 5 min-sum, config 2 DNA
     batch through the host API), shrunk: each has its own oracle check."""
     out = _bench("--batch-per-gpu", "1024", "--steps", "1", "--warmup", "0", "--cpu-seconds", "0.5",
-                 "--msa-batch", "8192")
+                 "--msa-batch", "8192", "--hbm-batch", "2048")
     sec = out["secondary"]
     m = sec["config5_msa_1m"]
     assert m["batch"] == 8192 and m["compressed_msa"] and m["check"]["mismatches"] == 0 and m["check"]["checked"] >= 8
@@ -59,6 +59,12 @@ def test_bench_secondary_legs(gpu):
     assert f["same_as_coded"] and f["value"] > 0 and f["batch"] == 1024
     assert out["config"]["input"].startswith("int8") and "true>" in out["roofline"]["kernels"]["variable"]
     assert "false>" in f["kernels"]["variable"]
+    # the headline's kernels streaming from HBM: one pass over every tile, nothing resident
+    h = sec["config3_hbm_streaming"]
+    assert h["batch"] == 2048 and not h["schedule"]["resident_pool"] and h["schedule"]["group_tiles"] == 32
+    assert h["check"]["mismatches"] == 0 and h["check"]["checked"] == 16 and h["roofline"]["achieved"] > 0
+    assert h["roofline"]["kernel"].startswith("k_check_bp<72,true,false>") or \
+        h["roofline"]["kernel"].startswith("k_var_m<false,8,true,true")
 
 
 def test_bench_dna272_line(gpu):
