@@ -709,9 +709,14 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
         for (int s = 0; s < DV; ++s) eid[c][s] = col_edge[(size_t)(j0 + c) * DV + s];
     double l[CPW][DV], pv[CPW], xin[CPW];
     int8_t kin[CPW];  // PC: the refilled lane's input codes
-    bool bad_in = false;  // a refilled lane's out-of-range index (reported at the end)
+    // a refilled lane's out-of-range index, reported at the end: held in a
+    // VGPR (opaque copy below), as a lane mask in SGPRs it pushed
+    // k_var_msa_c past 96 SGPRs (6 instead of 7 waves per SIMD, config 5 -3 %)
+    bool bad_in = false;
+    int bad_v = 0;
     if (fr) {  // refilled lane: its input row, prefetched with the c2v loads
         const size_t rb = (size_t)refill_row(rf.lane_b[t * TILE + lane], rf, bad_in) * N;
+        bad_v = bad_in ? 1 : 0;
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             if constexpr (PC) kin[c] = rf.in_code[rb + j0 + c];
@@ -833,7 +838,8 @@ __device__ __forceinline__ void var_m_block(typename Msg<INPLACE>::in c2v_t, typ
     // the reports of skipped accesses: the lane's pool slot (the indices need
     // not stay live; cont_lanes reports an out-of-range index itself)
     if (CONT && fl && !fok) lane_fault(rf.fault, kFaultOutput, t * TILE + lane);
-    if (bad_in) lane_fault(rf.fault, kFaultRefill, t * TILE + lane);
+    asm volatile("" : "+v"(bad_v));
+    if (bad_v) lane_fault(rf.fault, kFaultRefill, t * TILE + lane);
 }
 
 template <bool MSA, int DV, bool NT, bool CONT, int CPW, bool INPLACE, bool PC = false>
@@ -1247,8 +1253,10 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
     double l[CPW][DV], pv[CPW], xin[CPW];
     int8_t kin[CPW];  // PC: the refilled lane's input codes
     bool bad_in = false;  // as k_var_m
+    int bad_v = 0;
     if (fr) {
         const size_t rb = (size_t)refill_row(rf.lane_b[t * TILE + lane], rf, bad_in) * N;
+        bad_v = bad_in ? 1 : 0;
 #pragma unroll
         for (int c = 0; c < CPW; ++c) {
             if constexpr (PC) kin[c] = rf.in_code[rb + j0 + c];
@@ -1390,7 +1398,8 @@ __global__ __launch_bounds__(256) void k_var_msa_c(const double* __restrict__ re
     // the reports of skipped accesses: the lane's pool slot (the indices need
     // not stay live; cont_lanes reports an out-of-range index itself)
     if (CONT && fl && !fok) lane_fault(rf.fault, kFaultOutput, t * TILE + lane);
-    if (bad_in) lane_fault(rf.fault, kFaultRefill, t * TILE + lane);
+    asm volatile("" : "+v"(bad_v));
+    if (bad_v) lane_fault(rf.fault, kFaultRefill, t * TILE + lane);
 }
 
 // ---------------------------------------------------------------------------
