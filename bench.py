@@ -104,7 +104,8 @@ def parse():
                     help="single-fill BP: first check from the prior (LDPC_SCHED_FIRST_FROM_PRIOR; -1: engine default)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
     ap.add_argument("--secondary", type=int, default=1,
-                    help="N = 1: also time config 2 (DNA batch, host API) and config 5 (1M min-sum) after the headline")
+                    help="N = 1: also time the headline on fp64 input and streaming from HBM, config 5 (1M min-sum) "
+                         "and config 2 (DNA batch, host API) after the headline")
     ap.add_argument("--msa-batch", type=int, default=1_000_000, help="config-5 secondary leg: codewords")
     ap.add_argument("--hbm-batch", type=int, default=16384,
                     help="HBM-streaming secondary leg: codewords in its one pass (0: skip the leg)")
