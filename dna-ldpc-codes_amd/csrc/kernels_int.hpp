@@ -6,8 +6,9 @@
 //
 //   quantized / offset min-sum  Run_MSA_Decoder dec.cpp:1174-1210 with
 //     Init_MSA :1256-1298, Check_Update_MSA :1357-1396 (offset beta, clip at
-//     0), Variable_Update_MSA :1438-1477 (the bSave_word_state trapping-set
-//     post-processing branch is a debugging mode and is not reproduced),
+//     0), Variable_Update_MSA :1438-1477 (its bSave_word_state trapping-set
+//     post-processing branch is unreachable in the reference build: the flag
+//     is set FALSE at DNA_main.cpp:697 and never TRUE, :724 is commented out),
 //     Decision_MSA :1624-1656, Set_MSA :1683-1701, Cal_MSA_Q :1708-1746,
 //     Cal_MSA_Clip :1748-1764.
 //   Gallager A / B1 / B2        Run_Gallager_Decoder dec.cpp:699-723,
