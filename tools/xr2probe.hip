@@ -22,6 +22,8 @@
 //   variable  task (codeword, column block b): lane = column, its 8 edges
 //             (one per row block, ascending row) coalesced, dec.cpp:667-693,
 //             the decision ballots
+//   parts     (C = 3) the check task without its 147 KB load / store, and
+//             with only them
 //   barrier   per XCD: every wave drains its stores, one agent-scope atomic
 //             add per workgroup, a bounded relaxed poll; message loads are
 //             agent-scope (sc1: they miss the CU's L1 and hit the XCD's L2)
@@ -161,31 +163,37 @@ __global__ __launch_bounds__(256, 1) void k_xr2(Args a)
             double* blk = a.msg + ((size_t)c * RB + t) * CB * Q;
             const auto rb = rsrc(blk, (uint64_t)CB * Q * 8);
             // the block's 147 KB: thread tid loads elements tid + 256 q (512-B wave segments)
+            if (!(a.mode & 4)) {
 #pragma unroll 24
-            for (int q = 0; q < CB * Q / 256; ++q) s_blk[tid + 256 * q] = ld_l2(rb, (uint32_t)(tid + 256 * q) * 8);
+                for (int q = 0; q < CB * Q / 256; ++q) s_blk[tid + 256 * q] = ld_l2(rb, (uint32_t)(tid + 256 * q) * 8);
+            }
             const auto rh = rsrc(a.hard + (size_t)c * (NCOL / 64), NCOL / 8);
             for (int q = tid; q < NCOL / 64; q += 256)
                 s_hb[q] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rh, q * 8, 0, kSc1));
             if (tid == 0) s_any = 0;
             __syncthreads();
-            const uint16_t* ix = a.ridx + (size_t)t * DC * Q + tid;
-            uint16_t id[DC];
+            if (!(a.mode & 8)) {
+                const uint16_t* ix = a.ridx + (size_t)t * DC * Q + tid;
+                uint16_t id[DC];
 #pragma unroll
-            for (int k = 0; k < DC; ++k) id[k] = ix[(size_t)k * Q];
-            double xv[DC];
-            unsigned par = 0;
+                for (int k = 0; k < DC; ++k) id[k] = ix[(size_t)k * Q];
+                double xv[DC];
+                unsigned par = 0;
 #pragma unroll
-            for (int k = 0; k < DC; ++k) {
-                xv[k] = s_blk[id[k]];
-                par ^= (unsigned)(s_hb[id[k] >> 6] >> (id[k] & 63)) & 1u;
+                for (int k = 0; k < DC; ++k) {
+                    xv[k] = s_blk[id[k]];
+                    par ^= (unsigned)(s_hb[id[k] >> 6] >> (id[k] & 63)) & 1u;
+                }
+                check_row(xv);
+                if (__ballot(par) && lane == 0) atomicOr(&s_any, 1u);
+#pragma unroll
+                for (int k = 0; k < DC; ++k) s_blk[id[k]] = xv[k];
             }
-            check_row(xv);
-            if (__ballot(par) && lane == 0) atomicOr(&s_any, 1u);
-#pragma unroll
-            for (int k = 0; k < DC; ++k) s_blk[id[k]] = xv[k];
             __syncthreads();
+            if (!(a.mode & 4)) {
 #pragma unroll 8
-            for (int q = 0; q < CB * Q / 256; ++q) blk[tid + 256 * q] = s_blk[tid + 256 * q];
+                for (int q = 0; q < CB * Q / 256; ++q) blk[tid + 256 * q] = s_blk[tid + 256 * q];
+            }
         }
         if (!xcd_barrier(a, x, nwg, ++e)) return;
         // ---- variable phase: tasks (codeword, column block), strided over the XCD's workgroups ----
@@ -295,9 +303,13 @@ int main(int argc, char** argv)
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     std::printf("xr2probe: %d codewords max, %zu B LDS per workgroup\n", ncw, (size_t)(CB * Q * 8 + NCOL / 8 + 4));
-    const char* mname[] = {"barriers", "check", "variable", "both"};
+    // mode bits: 1 check phase, 2 variable phase; 4: the check task without
+    // its 147 KB load and store (LDS reads, arithmetic, LDS writes only),
+    // 8: the check task's load and store only
+    const char* mname[] = {"barriers", "check", "variable", "both", "", "chk-lds+arith", "", "", "", "chk-ld/st"};
     for (int C : {1, 2, 3, 4}) {
-        for (int mode : {0, 1, 2, 3}) {
+        for (int mode : {0, 1, 2, 3, 5, 9}) {
+            if ((mode == 5 || mode == 9) && C != 3) continue;
             float ms[2];
             const int its[2] = {4, 24};
             for (int r = 0; r < 2; r++) {
