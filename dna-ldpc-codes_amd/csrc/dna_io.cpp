@@ -12,7 +12,7 @@
 #include <string>
 
 #include "../../include/ldpc_amd.h"
-#include "engine.hpp"
+#include "host_io.hpp"
 
 namespace ldpc {
 

@@ -36,6 +36,10 @@ int build_graph(int32_t M, int32_t N, const int32_t* rows, const int32_t* cols, 
         if (msg) *msg = "graph dimensions must be positive";
         return LDPC_ERR_ARG;
     }
+    if (M > LDPC_MAX_DIM || N > LDPC_MAX_DIM) {
+        if (msg) *msg = "graph dimensions above LDPC_MAX_DIM";
+        return LDPC_ERR_UNSUPPORTED;
+    }
     std::vector<uint64_t> key((size_t)n);
     for (int64_t i = 0; i < n; i++) {
         if (rows[i] < 0 || rows[i] >= M || cols[i] < 0 || cols[i] >= N) {
@@ -114,6 +118,10 @@ int load_pchk(const std::string& path, HostGraph& g, std::string* msg)
     if (!next(&M) || M <= 0 || !next(&N) || N <= 0) {
         if (msg) *msg = "Error reading parity check matrix from " + path;  // rcode.cpp:75-79
         return LDPC_ERR_FORMAT;
+    }
+    if (M > LDPC_MAX_DIM || N > LDPC_MAX_DIM) {
+        if (msg) *msg = "Parity check matrix in " + path + " is larger than LDPC_MAX_DIM";
+        return LDPC_ERR_UNSUPPORTED;
     }
     std::vector<int32_t> rows, cols;
     rows.reserve(nwords);
@@ -215,6 +223,9 @@ int load_alist(const std::string& path, bool transpose, HostGraph& g, std::strin
     if (sc.next(&M) != 1 || M < 1 || sc.next(&N) != 1 || N < 1 || sc.next(&mxrw) != 1 || mxrw < 0 || mxrw > N ||
         sc.next(&mxcw) != 1 || mxcw < 0 || mxcw > M)
         return bad();
+    // the M + N degrees that follow take two bytes each at least: a header
+    // larger than the file cannot be right, and must not size the allocations
+    if ((size_t)M + (size_t)N > sc.buf.size() / 2) return bad();
     std::vector<int> rw((size_t)M), cw((size_t)N);
     for (int i = 0; i < M; i++)
         if (sc.next(&rw[(size_t)i]) != 1 || rw[(size_t)i] < 0 || rw[(size_t)i] > N) return bad();

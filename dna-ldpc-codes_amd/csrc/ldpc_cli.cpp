@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "../../include/ldpc_amd.h"
+#include "cli_io.hpp"
 
 static void die(const char* msg)
 {
@@ -44,23 +45,9 @@ static void die(const char* msg)
     std::exit(1);
 }
 
-static bool read_tokens(const std::string& path, std::vector<std::string>& out, size_t need)
-{
-    FILE* f = std::fopen(path.c_str(), "rb");
-    if (!f) return false;
-    std::string cur;
-    int ch;
-    while ((ch = std::fgetc(f)) != EOF && out.size() < need) {
-        if (ch == ' ' || ch == '\n' || ch == '\r' || ch == '\t') {
-            if (!cur.empty()) { out.push_back(cur); cur.clear(); }
-        } else {
-            cur.push_back((char)ch);
-        }
-    }
-    if (!cur.empty() && out.size() < need) out.push_back(cur);
-    std::fclose(f);
-    return true;
-}
+// bounds on argv-sized work that the reference leaves unchecked
+constexpr long long kMaxSideInts = 1LL << 24;   // entries of an SC-code side file
+constexpr long long kMaxFrames = 1LL << 40;     // frame counters stay far from int64 overflow
 
 int main(int argc, char** argv)
 {
@@ -96,14 +83,11 @@ int main(int argc, char** argv)
     if (shortening == 1) { s_start = std::atoi(arg()); s_end = std::atoi(arg()); }
     if (shortening == 2) { s_etha = std::atoi(arg()); s_num = std::atoi(arg()); }
     if (targeting) { target_VN[0] = std::atoi(arg()); target_VN[1] = std::atoi(arg()); }
-    auto read_ints = [&](const std::string& path, int n, std::vector<int>& out) {
-        std::vector<std::string> tok;
-        if (n > 0 && !read_tokens(path, tok, (size_t)n)) {
-            std::fprintf(stderr, "ldpc: cannot open %s\n", path.c_str());
-            std::exit(1);
-        }
+    auto read_ints = [&](const std::string& path, long long n, std::vector<int>& out) {
         // a short file leaves the calloc'd zeros, as fscanf does
-        for (int i = 0; i < n; i++) out.push_back(i < (int)tok.size() ? std::atoi(tok[(size_t)i].c_str()) : 0);
+        std::string msg;
+        if (n > kMaxSideInts) die("ldpc: SC-code side file length out of range");
+        if (!ldpc_cli::read_int_file(path, (size_t)n, /*allow_short=*/true, out, &msg)) die(("ldpc: " + msg).c_str());
     };
     if (punct >= 2 && punct <= 4) {
         // SetUp :355-431: [start1 end1 (type 4)] w L, <pchk>.txt holds D = L + w - 1
@@ -111,7 +95,7 @@ int main(int argc, char** argv)
         if (punct == 4) { p_start1 = std::atoi(arg()); p_end1 = std::atoi(arg()); }
         sc_w = std::atoi(arg());
         sc_L = std::atoi(arg());
-        const int D = sc_L + sc_w - 1;
+        const long long D = (long long)sc_L + sc_w - 1;
         if (sc_L < 0 || D < 0 || (D < sc_L)) die("ldpc: SC-code w / L out of range");
         read_ints(pchk_base + ".txt", D, sc_M);
         if (punct >= 3) { p_start2 = std::atoi(arg()); p_end2 = std::atoi(arg()); }
@@ -150,17 +134,19 @@ int main(int argc, char** argv)
     std::printf("g_CODE_M : %d\n", M);
     std::printf("\n");
     if (!targeting) { target_VN[0] = 1; target_VN[1] = N; }
+    // LDPC_BIT_Check indexes codeword[target_VN[0]-1 .. target_VN[1]-1] unchecked (DNA_main.cpp:1675-1706)
+    if (target_VN[0] < 1 || target_VN[1] > N || target_VN[0] > target_VN[1]) die("ldpc: target_VN range outside the code");
     double rate;  // Set_Code :565-605 (g_rand_type = RAND_SEED, g_save_type = 0 in this build)
     if (punct == 1) {
-        const double np = (double)(p_end - p_start + 1);
+        const double np = (double)p_end - p_start + 1;
         rate = 1.0 - ((double)M - np) / ((double)N - np);
     } else if (punct >= 2 && punct <= 4) {
-        int np = (p_end - p_start + 1) * sc_L;
-        if (punct >= 3) np += p_end2 - p_start2 + 1;
-        if (punct == 4) np += (p_end1 - p_start1 + 1) * (sc_w - 1);
+        long long np = ((long long)p_end - p_start + 1) * sc_L;
+        if (punct >= 3) np += (long long)p_end2 - p_start2 + 1;
+        if (punct == 4) np += ((long long)p_end1 - p_start1 + 1) * (sc_w - 1);
         rate = 1.0 - (double)(M - np) / (double)(N - np);
     } else if (shortening == 1) {
-        rate = 1.0 - (double)M / (double)(N - (s_end - s_start + 1));
+        rate = 1.0 - (double)M / ((double)N - ((double)s_end - s_start + 1));
     } else if (shortening == 2) {
         if (s_etha == 0) die("ldpc: shortening type 2 needs a nonzero period");
         const int ns = (int)(s_num * std::floor((double)sc_L / (double)s_etha));
@@ -174,16 +160,14 @@ int main(int argc, char** argv)
     std::time(&t_start);
 
     // ---- LDPC_Encode: read codeword + LLR (DNA_main.cpp:1319-1345) ----
-    std::vector<std::string> tok_cw, tok_soft;
-    if (!read_tokens(file_cw, tok_cw, (size_t)N)) { std::fprintf(stderr, "ldpc: cannot open %s\n", file_cw.c_str()); return 1; }
-    if (!read_tokens(file_soft, tok_soft, (size_t)N)) { std::fprintf(stderr, "ldpc: cannot open %s\n", file_soft.c_str()); return 1; }
-    if ((int)tok_cw.size() < N || (int)tok_soft.size() < N) die("ldpc: input file shorter than the code length");
-    std::vector<int> codeword((size_t)N);
-    std::vector<double> llr((size_t)N);
-    for (int i = 0; i < N; i++) {
-        codeword[(size_t)i] = std::atoi(tok_cw[(size_t)i].c_str());
-        llr[(size_t)i] = std::strtod(tok_soft[(size_t)i].c_str(), nullptr);  // fscanf %lf
-    }
+    // cli_io.hpp: a missing file, fewer than N values or a non-numeric token
+    // exit 1 (the reference runs on with stale or zero values)
+    std::vector<int> codeword;
+    std::vector<double> llr;
+    std::string io_msg;
+    if (!ldpc_cli::read_int_file(file_cw, (size_t)N, /*allow_short=*/false, codeword, &io_msg) ||
+        !ldpc_cli::read_double_file(file_soft, (size_t)N, llr, &io_msg))
+        die(("ldpc: " + io_msg).c_str());
 
     // ---- LDPC_Channel raw error count (DNA_main.cpp:1711-1748) ----
     const int len_raw = bSystematic ? K : N;
@@ -249,6 +233,7 @@ int main(int argc, char** argv)
     } else {
         frames = frame_num;
     }
+    if (frames > kMaxFrames) die("ldpc: frame_num out of range");
     long long frame_i[3] = {frames, frames, 0};
     long long bit_errs[3] = {raw * frames, bit_err * frames, bit_err * frames};
     long long frame_errs[3] = {raw > 0 ? frames : 0, bit_err > 0 ? frames : 0, bit_err > 0 ? frames : 0};

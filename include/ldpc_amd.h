@@ -143,6 +143,13 @@ typedef struct ldpc_opts {
 /* Graph                                                                     */
 /* ------------------------------------------------------------------------ */
 
+/* Largest M or N a graph may have (every constructor below returns
+ * LDPC_ERR_UNSUPPORTED above it).  The reference allocates whatever a file's
+ * header asks for (mod2sparse_allocate via mod2sparse_read,
+ * mod2sparse.cpp:381-400); a 12-byte .pchk could otherwise make the host
+ * allocate and clear 16 GB of row/column pointers. */
+#define LDPC_MAX_DIM (1 << 26)
+
 /* Load a Radford-Neal .pchk file.  Replaces read_pchk (rcode.cpp:54-85) +
  * mod2sparse_read (mod2sparse.cpp:381-427): same magic ('P'<<8)+0x80, same
  * record stream, same row/column ordering and duplicate rule

@@ -86,6 +86,7 @@ int oracle_graph_load(const char *path, oracle_graph *g)
         if (eof) break;                       /* EOF before terminator: error */
         if (v == 0) { ok = 1; break; }
         if (v < 0) {
+            if (v == INT32_MIN) break;        /* -v overflows: the reference's row -v-1 wraps out of range */
             row = -v - 1;
             if (row >= M) break;
         } else {

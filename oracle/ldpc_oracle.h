@@ -29,10 +29,6 @@ int oracle_msa(const oracle_graph *g, const double *LLR, int max_iter, uint8_t *
 int oracle_decode_batch(const oracle_graph *g, const double *llr, int64_t B, int max_iter, int algo,
                         int post_mode, int nthreads, uint8_t *hard, double *post, int32_t *iters, uint8_t *valid);
 
-#ifdef __cplusplus
-}
-#endif
-
 /* Integer-message decoders of dec.cpp (test oracle for LDPC_ALGO_QMSA and
  * LDPC_ALGO_GALLAGER_*; algo 2 = quantized/offset min-sum Run_MSA_Decoder
  * dec.cpp:1174, 3/4/5 = Run_Gallager_Decoder dec.cpp:699 type 0/1/2).
@@ -42,5 +38,10 @@ int oracle_decode_batch(const oracle_graph *g, const double *llr, int64_t B, int
 int oracle_decode_int_batch(const oracle_graph *g, const double *llr, int64_t B, int max_iter, int algo,
                             int precision, double step, int beta, uint64_t seed, int nthreads,
                             uint8_t *hard, double *post, int32_t *iters, uint8_t *valid);
+
+#ifdef __cplusplus
+}
+#endif
+
 
 #endif

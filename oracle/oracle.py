@@ -152,19 +152,37 @@ class RefGraph:
 
     _lib = None
 
-    def __init__(self, path: str):
+    @staticmethod
+    def _load_lib():
         if RefGraph._lib is None:
             L = C.CDLL(os.path.join(_HERE, "_ref", "libref.so"))
             L.ref_load.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+            L.ref_try_load.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
             L.ref_rows.argtypes = [C.c_void_p, C.c_void_p]
             L.ref_rows.restype = C.c_int64
             L.ref_cols.argtypes = [C.c_void_p, C.c_void_p]
             L.ref_cols.restype = C.c_int64
             L.ref_check.argtypes = [C.c_void_p, C.c_void_p]
             RefGraph._lib = L
+        return RefGraph._lib
+
+    def __init__(self, path: str):
         M, N = C.c_int(), C.c_int()
-        RefGraph._lib.ref_load(path.encode(), C.byref(M), C.byref(N))
+        RefGraph._load_lib().ref_load(path.encode(), C.byref(M), C.byref(N))
         self.M, self.N = M.value, N.value
+
+    @classmethod
+    def try_load(cls, path: str):
+        """read_pchk's steps without its exit() (ref_harness.cpp ref_try_load):
+        (rc, graph) with rc 0 accepted, -1 open, -2 magic, -3 records.  The
+        reference allocates what the header asks for: keep M and N small."""
+        M, N = C.c_int(), C.c_int()
+        rc = cls._load_lib().ref_try_load(path.encode(), C.byref(M), C.byref(N))
+        if rc != 0:
+            return rc, None
+        g = cls.__new__(cls)
+        g.M, g.N = M.value, N.value
+        return 0, g
 
     def rows(self, E_hint: int):
         deg = np.zeros(self.M, np.int32)

@@ -19,6 +19,7 @@
 #include "mod2sparse.h"
 #include "rcode.h"
 #include "check.h"
+#include "intio.h"
 
 extern "C" {
 
@@ -29,6 +30,31 @@ int ref_load(const char *path, int *M_out, int *N_out)
     read_pchk((char *)path);
     *M_out = mod2sparse_rows(H);
     *N_out = mod2sparse_cols(H);
+    return 0;
+}
+
+// read_pchk's own steps without its exit(): the magic word through intio_read,
+// then mod2sparse_read (rcode.cpp:60-79).  0 = accepted (H replaced),
+// -1 = cannot open, -2 = wrong magic, -3 = mod2sparse_read refused the
+// records.  mod2sparse_read allocates whatever the header asks for and
+// chk_alloc exits when that fails, so callers keep M and N small.
+int ref_try_load(const char *path, int *M_out, int *N_out)
+{
+    FILE *f = fopen(path, "rb");
+    if (!f) return -1;
+    if (intio_read(f) != ('P' << 8) + 0x80) {
+        fclose(f);
+        return -2;
+    }
+    mod2sparse *h = mod2sparse_read(f);
+    fclose(f);
+    if (!h) return -3;
+    if (H) mod2sparse_free(H);
+    H = h;
+    M = mod2sparse_rows(H);
+    N = mod2sparse_cols(H);
+    *M_out = M;
+    *N_out = N;
     return 0;
 }
 

@@ -1,0 +1,294 @@
+"""Host sanitizer row ("host ASan/UBSan build of the C++
+side"), CPU only.
+
+tests/asan/Makefile builds the product's host-only units -- the .pchk / alist
+readers and writers and RS-LDPC construction (graph.cpp), the lattice encoder
+(host_simd.cpp), the CLI's codeword / soft / side-file readers (cli_io.cpp)
+and the soft-file writer (dna_io.cpp) -- plus the oracle (oracle/ldpc_oracle.c)
+with AddressSanitizer, LeakSanitizer and UndefinedBehaviorSanitizer, every
+report fatal, into tests/asan/build/host_check.  These tests feed it malformed
+inputs and require zero sanitizer reports and zero disagreements:
+
+* .pchk: the product loader and the oracle's restatement must accept / refuse
+  every file together and build the same arrays, and the refusals must be the
+  reference's own (mod2sparse_read via oracle/_ref, where it is built).  The
+  reference reads these files unchecked (rcode.cpp:54-85: a header M or N
+  sizes its allocation, whatever the file length); LDPC_MAX_DIM refuses
+  oversized headers before anything is allocated.
+* alist: product refusals against the reference's alist-to-pchk exit status.
+* codeword / soft files (DNA_main.cpp:1322-1345 reads them with unchecked
+  fscanf): short, long, non-numeric, NaN / inf, oversized tokens.
+* seeded mutation runs over all three formats, one oracle BP and min-sum
+  decode, the integer decoders, RS-LDPC construction, py_float_repr.
+
+Regression cases for what building this row turned up (the sanitized runs
+themselves came back clean; these were found reading the inputs' paths): an
+INT32_MIN row record (-v overflows in the oracle's loader -- gcc folds -v-1
+to ~v before UBSan instruments it, so only the case catches it), headers
+above LDPC_MAX_DIM (a 12-byte .pchk made the host allocate and clear 16 GB),
+alist headers larger than the file, the C++ linkage of
+oracle_decode_int_batch (ldpc_oracle.h), target_VN outside the code (the CLI
+indexed the codeword out of bounds) and non-numeric input tokens (atoi / strtod
+read them as 0).
+"""
+import os
+import shutil
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PCHK, ROOT
+
+ASAN_DIR = os.path.join(ROOT, "tests", "asan")
+HOST_CHECK = os.path.join(ASAN_DIR, "build", "host_check")
+REF_A2P = os.path.join(ROOT, "oracle", "_ref", "alist-to-pchk")
+CLI = os.path.join(ROOT, "dna-ldpc-codes_amd", "bin", "ldpc")
+MAGIC = (ord("P") << 8) + 0x80
+LDPC_MAX_DIM = 1 << 26
+LDPC_ERR_IO, LDPC_ERR_FORMAT, LDPC_ERR_UNSUPPORTED = -2, -3, -5  # include/ldpc_amd.h
+
+SAN_ENV = {
+    "ASAN_OPTIONS": "detect_leaks=1:halt_on_error=1:abort_on_error=0:exitcode=97:strict_string_checks=1",
+    "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1:exitcode=98",
+}
+
+
+@pytest.fixture(scope="module")
+def hc():
+    if shutil.which("g++") is None:
+        pytest.skip("no host C++ compiler")
+    subprocess.run(["make", "-s", "-C", ASAN_DIR], check=True, capture_output=True, timeout=600)
+    assert os.access(HOST_CHECK, os.X_OK)
+
+    def run(*args, cwd=None):
+        env = dict(os.environ, **SAN_ENV)
+        r = subprocess.run([HOST_CHECK, *map(str, args)], capture_output=True, text=True, env=env, cwd=cwd,
+                           timeout=300)
+        report = r.stderr
+        assert "Sanitizer" not in report and "runtime error" not in report, report[-4000:]
+        assert r.returncode == 0, (r.returncode, r.stdout[-2000:], report[-2000:])
+        assert "MISMATCH" not in r.stdout, r.stdout
+        return r.stdout.strip().splitlines()
+
+    return run
+
+
+def _words(*ws):
+    return b"".join(struct.pack("<i", w) for w in ws)
+
+
+# (name, bytes, accepted?) -- the reference's mod2sparse_read rules
+# (mod2sparse.cpp:381-427): M, N > 0; -(r+1) selects row r < M; c+1 inserts
+# column c < N into the current row; 0 terminates; EOF first is an error.
+PCHK_CASES = [
+    ("empty", b"", False),
+    ("three_bytes", b"\x80P\x00", False),
+    ("magic_only", _words(MAGIC), False),
+    ("wrong_magic", _words(MAGIC + 1, 2, 3, -1, 1, 0), False),
+    ("m_zero", _words(MAGIC, 0, 3, 0), False),
+    ("n_negative", _words(MAGIC, 2, -1, 0), False),
+    ("no_records", _words(MAGIC, 2, 3), False),
+    ("terminator_only", _words(MAGIC, 2, 3, 0), True),
+    ("minimal", _words(MAGIC, 2, 3, -1, 1, 3, -2, 2, 0), True),
+    ("column_eq_n", _words(MAGIC, 2, 3, -1, 4, 0), False),
+    ("row_eq_m", _words(MAGIC, 2, 3, -3, 1, 0), False),
+    ("column_before_row", _words(MAGIC, 2, 3, 1, -1, 0), False),
+    ("int32_min_row", _words(MAGIC, 2, 3, -(1 << 31), 1, 0), False),
+    ("int32_max_col", _words(MAGIC, 2, 3, -1, (1 << 31) - 1, 0), False),
+    ("missing_terminator", _words(MAGIC, 2, 3, -1, 1, 2), False),
+    ("partial_word_before_end", _words(MAGIC, 2, 3, -1, 1) + b"\x00\x00", False),
+    ("odd_tail_after_end", _words(MAGIC, 2, 3, -1, 1, 0) + b"\x07", True),
+    ("garbage_after_end", _words(MAGIC, 2, 3, -1, 1, 0, 99, -99) + b"xyz", True),
+    ("duplicates", _words(MAGIC, 2, 3, -1, 2, 2, 1, 2, -2, 3, -1, 2, 0), True),
+    ("descending", _words(MAGIC, 3, 4, -3, 4, 1, -1, 3, 2, -2, 4, 0), True),
+    ("row_reselected", _words(MAGIC, 2, 3, -1, 1, -2, 2, -1, 3, 0), True),
+    ("empty_row_selected", _words(MAGIC, 2, 3, -1, -2, 1, 0), True),
+    # headers above LDPC_MAX_DIM: refused before any allocation (the
+    # reference would calloc them; no reference comparison for these)
+    ("huge_m", _words(MAGIC, (1 << 31) - 1, 3, 0), None),
+    ("huge_n", _words(MAGIC, 2, LDPC_MAX_DIM + 1, -1, 1, 0), None),
+]
+
+
+@pytest.mark.parametrize("name,data,ok", PCHK_CASES, ids=[c[0] for c in PCHK_CASES])
+def test_pchk_malformed(hc, oracle_mod, tmp_path, name, data, ok):
+    f = tmp_path / f"{name}.pchk"
+    f.write_bytes(data)
+    out = hc("pchk", f)  # product vs oracle inside the sanitized build
+    assert len(out) == 1
+    if ok is None:
+        assert out[0].startswith(f"err pchk {LDPC_ERR_UNSUPPORTED} "), out
+        return
+    assert out[0].startswith("ok pchk" if ok else f"err pchk {LDPC_ERR_FORMAT} "), out
+    if oracle_mod.ref_available():  # the reference's own mod2sparse_read
+        rc, ref = oracle_mod.RefGraph.try_load(str(f))
+        assert (rc == 0) == ok, (name, rc)
+        if ok:
+            M, N, E = (int(v) for v in out[0].split()[2:5])
+            assert (ref.M, ref.N) == (M, N)
+            deg, _ = ref.rows(E + 8)
+            assert int(deg.sum()) == E
+
+
+def test_pchk_missing_file(hc, tmp_path):
+    assert hc("pchk", tmp_path / "nope.pchk")[0].startswith(f"err pchk {LDPC_ERR_IO} ")
+
+
+def test_pchk_dna_code(hc):
+    assert hc("pchk", PCHK) == ["ok pchk 2048 18432 147456"]
+
+
+def test_pchk_mutations(hc, tmp_path):
+    for seed in (1, 2, 3):
+        (line,) = hc("fuzz-pchk", seed, 600, tmp_path)
+        n_ok = int(line.split()[-2])
+        assert 0 < n_ok < 600, line  # both outcomes exercised
+
+
+def _alist(M, N, rows, cols):
+    """alist text with explicit degree and entry lists (1-based, 0 padding)."""
+    mr = max(len(r) for r in rows)
+    mc = max(len(c) for c in cols)
+    t = [f"{M} {N}", f"{mr} {mc}", " ".join(str(len(r)) for r in rows), " ".join(str(len(c)) for c in cols)]
+    t += [" ".join(str(v) for v in r + [0] * (mr - len(r))) for r in rows]
+    t += [" ".join(str(v) for v in c + [0] * (mc - len(c))) for c in cols]
+    return "\n".join(t) + "\n"
+
+
+GOOD = _alist(2, 3, [[1, 3], [2]], [[1], [2], [1]])
+ALIST_CASES = [
+    ("good", GOOD, True),
+    ("row_degree_disagrees", GOOD.replace("\n2 1\n", "\n1 1\n", 1), False),
+    ("entry_above_n", _alist(2, 3, [[1, 4], [2]], [[1], [2], [1]]), False),
+    ("duplicate_in_row", _alist(2, 3, [[1, 1], [2]], [[1, 1], [2], []]), False),
+    ("column_lists_disagree", _alist(2, 3, [[1, 3], [2]], [[1], [2], [2]]), False),
+    ("trailing_number", GOOD + "5\n", False),
+    ("trailing_garbage", GOOD + "x\n", False),
+    ("truncated", GOOD[:-4], False),
+    ("non_numeric", GOOD.replace("2 3", "2 x", 1), False),
+    ("m_zero", "0 3\n1 1\n", False),
+    ("negative_degree", GOOD.replace("\n2 1\n", "\n-2 1\n", 1), False),
+    ("padding_not_zero", _alist(2, 3, [[1, 3], [2]], [[1], [2], [1]]).replace("2 0", "2 2", 1), False),
+    ("huge_header", "2000000000 2000000000\n1 1\n1 1\n", False),
+]
+
+
+@pytest.mark.parametrize("name,text,ok", ALIST_CASES, ids=[c[0] for c in ALIST_CASES])
+def test_alist_malformed(hc, tmp_path, name, text, ok):
+    f = tmp_path / f"{name}.alist"
+    f.write_text(text)
+    out = hc("alist", f)
+    assert len(out) == 2
+    assert out[0].startswith("ok alist " if ok else f"err alist {LDPC_ERR_FORMAT} "), out
+    if os.path.exists(REF_A2P) and name != "huge_header":  # the reference converter's verdict
+        r = subprocess.run([REF_A2P, str(f), str(tmp_path / "ref.pchk")], capture_output=True, timeout=60)
+        assert (r.returncode == 0) == ok, (name, r.returncode, r.stderr)
+
+
+def test_alist_mutations(hc, tmp_path):
+    for seed in (1, 2, 3):
+        (line,) = hc("fuzz-alist", seed, 600, tmp_path)
+        assert int(line.split()[-2]) > 0, line
+
+
+N_TOK = 64
+
+
+@pytest.mark.parametrize("name,text,status", [
+    ("exact", "0 1 " * 32, "ok ints 64 32"),
+    ("long", "1 " * 100, "ok ints 64 64"),
+    ("short", "1 " * 63, "err ints"),
+    ("empty", "", "err ints"),
+    ("non_numeric", "1 " * 10 + "one " + "1 " * 60, "err ints"),
+    ("float_token", "1.0 " * 64, "err ints"),
+    ("overflow_saturates", "99999999999 " + "0 " * 63, f"ok ints 64 {2**31 - 1}"),
+    ("binary", "\x00\x01\x02" * 50, "err ints"),
+    ("separators", "1\t1\r\n1\v1\f" * 16, "ok ints 64 64"),
+    ("huge_token", "1" * 100000 + " " + "0 " * 63, "err ints"),
+])
+def test_codeword_file(hc, tmp_path, name, text, status):
+    f = tmp_path / "cw.txt"
+    f.write_bytes(text.encode("latin-1"))
+    (line,) = hc("ints", f, N_TOK, 0)
+    assert line.startswith(status), (name, line)
+
+
+def test_side_file_short_is_zero_padded(hc, tmp_path):
+    f = tmp_path / "side.txt"
+    f.write_text("5 6 7")
+    assert hc("ints", f, 10, 1) == ["ok ints 10 18"]  # SetUp's calloc'd zeros
+    assert hc("ints", tmp_path / "none.txt", 10, 1)[0].startswith("err ints cannot open")
+
+
+@pytest.mark.parametrize("name,text,status", [
+    ("repr_floats", " ".join(repr(float(v)) for v in np.linspace(-9, 9, 64)), "ok doubles 64 nan=0 inf=0 first=-9"),
+    ("nan_inf", "nan -inf inf -nan " + "0.5 " * 60, "ok doubles 64 nan=2 inf=2 first=nan"),
+    ("overflow", "1e999 " + "0 " * 63, "ok doubles 64 nan=0 inf=1 first=inf"),
+    ("hex_and_ints", "0x1p3 " + "7 " * 63, "ok doubles 64 nan=0 inf=0 first=8"),
+    ("short", "0.5 " * 10, "err doubles"),
+    ("non_numeric", "0.5 " * 30 + "1e " + "0.5 " * 40, "err doubles"),
+    ("comma", "0,5 " * 64, "err doubles"),
+    ("missing", None, "err doubles cannot open"),
+])
+def test_soft_file(hc, tmp_path, name, text, status):
+    f = tmp_path / "soft.txt"
+    if text is not None:
+        f.write_text(text)
+    (line,) = hc("doubles", f, N_TOK)
+    assert line.startswith(status), (name, line)
+
+
+def test_text_mutations(hc, tmp_path):
+    for seed in (1, 2):
+        (line,) = hc("fuzz-text", seed, 1500, tmp_path)
+        assert "ok fuzz-text" in line
+
+
+def test_repr_and_soft_writer(hc, tmp_path):
+    (line,) = hc("repr", 7, 3000, tmp_path)
+    assert line.startswith("ok repr")
+    assert sorted(os.listdir(tmp_path)) == [f"soft7_n18432_m1860_{i}.txt" for i in (1, 2, 3)]
+
+
+def test_lattice_encoder(hc):
+    assert hc("lattice", 11) == ["ok lattice"]
+
+
+def test_rs_ldpc_construction(hc):
+    out = hc("rs")
+    assert "ok rs 8 72 8 E=147456" in out and "ok rs 3 6 3 E=144" in out
+    assert sum(1 for l in out if l.startswith("err rs")) == 7
+
+
+@pytest.mark.parametrize("algo,p", [(0, 0.02), (1, 0.01), (0, 0.001)])
+def test_oracle_decode_sanitized(hc, algo, p):
+    out = hc("decode", PCHK, algo, 4, 3, p)
+    assert out[0].startswith(f"ok decode algo={algo} ")
+    assert sum(1 for l in out if l.startswith("ok decode-int")) == 4
+    if p == 0.001:  # a light BSC word converges to the all-zero codeword
+        assert "valid=1" in out[0] and "ones=0 syndrome=0" in out[0]
+
+
+def test_cli_refuses_bad_inputs(tmp_path):
+    """bin/ldpc exits 1 with a message before any decode (no GPU needed)."""
+    if not os.access(CLI, os.X_OK):
+        pytest.skip("bin/ldpc not built")
+    d = tmp_path
+    shutil.copyfile(PCHK, d / "decode_n18432_m2048_final.pchk")
+    (d / "cw.txt").write_text("0 " * 18432)
+    (d / "soft.txt").write_text("3.89 " * 18431 + "abc ")
+    (d / "short.txt").write_text("3.89 " * 100)
+    base = [CLI, "0", "0", "0", "7", "5", "1", "cw"]
+    tail = ["decode_n18432_m2048_final", "0", "0", "0"]
+    cases = [
+        (base + ["soft"] + tail + ["0"], "token 18432 is not a number"),
+        (base + ["short"] + tail + ["0"], "100 values, the code needs 18432"),
+        (base + ["missing"] + tail + ["0"], "cannot open missing.txt"),
+        (base + ["short"] + tail + ["1", "5", "99999"], "target_VN range outside the code"),
+        (base + ["short"] + tail + ["1", "0", "5"], "target_VN range outside the code"),
+    ]
+    for argv, msg in cases:
+        r = subprocess.run(argv, cwd=d, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 1 and msg in r.stderr, (argv, r.returncode, r.stderr)
