@@ -264,14 +264,25 @@ def moved_bytes(eng, N, M, E, coded=False) -> dict:
     return b
 
 
-def bound_detail(eng, coded=False) -> str:
+MALL_BYTES = 256 * 2 ** 20  # MI355X Infinity Cache (MALL)
+
+
+def bound_label(eng) -> str:
+    """roofline.bound: where the dominant kernel's bytes come from.  The
+    resident pool (~226 MB) lives in the 256 MB Infinity Cache, so its frac is
+    of bytes served by HBM and the MALL together; every
+    other schedule streams its messages from HBM."""
+    return "hbm+mall (resident pool)" if eng.resident else "hbm"
+
+
+def bound_detail(eng, coded=False, E=147456) -> str:
     note = (" Coded input: the variable kernel reads each column's prior as a 1-byte code (+ a 2 KB table), "
             "7 B per column and codeword-iteration fewer than the algorithmic (fp64 prior) bytes that `achieved` "
             "counts; `achieved_moved` counts the code." if coded and eng.continuous else "")
-    return _bound_detail(eng) + note
+    return _bound_detail(eng, E) + note
 
 
-def _bound_detail(eng) -> str:
+def _bound_detail(eng, E=147456) -> str:
     if eng.msa_compressed:
         return ("compressed min-sum (DESIGN.md sec. 4.2, 6.1), v2c in column order: the check kernel gathers its "
                 "8-tile group's v2c (604 MB, more than the 256 MB Infinity Cache) from HBM as 512-B segments; the "
@@ -283,11 +294,22 @@ def _bound_detail(eng) -> str:
                 "fabric interface once per phase (PMC fabric bytes = 1.02-1.04 x algorithmic), served by HBM and the "
                 "Infinity Cache; the DRAM-request counters count cache hits too on gfx950 (calibrated), so the cache "
                 "share is not observable; no MFMA")
-    if eng.group_tiles * 64 * 147456 * 8 > 256 * 2 ** 20:
-        return ("one grouped pass over every tile: the c2v scratch and the v2c stream (nontemporal) both exceed the "
-                "256 MB Infinity Cache, so every message byte streams from HBM; memory-bound, no MFMA")
-    return ("grouped schedule: the group's c2v scratch is meant to stay in the Infinity Cache between the phases, the "
-            "v2c stream goes to HBM (nontemporal); memory-bound, no MFMA")
+    tiles = -(-eng.cap // 64)  # tiles of one pass
+    group = tiles if eng.group_tiles < 0 else min(eng.group_tiles, tiles)
+    group_mb = group * 64 * E * 8 / 2 ** 20  # the group's fp64 c2v scratch
+    if group >= tiles:
+        return (f"one grouped pass over every tile ({tiles}): the c2v scratch ({group_mb:.0f} MB) and the v2c "
+                "stream (nontemporal) both exceed the 256 MB Infinity Cache, so every message byte streams from "
+                "HBM; memory-bound, no MFMA" if group_mb * 2 ** 20 > MALL_BYTES else
+                f"one grouped pass over every tile ({tiles}): the c2v scratch ({group_mb:.0f} MB) fits the 256 MB "
+                "Infinity Cache, the v2c stream goes to HBM (nontemporal); memory-bound, no MFMA")
+    if group_mb * 2 ** 20 > MALL_BYTES:
+        return (f"grouped schedule, {group} of {tiles} tiles per group: the group's c2v scratch ({group_mb:.0f} MB) "
+                "exceeds the 256 MB Infinity Cache, so it streams from HBM between the phases, as does the v2c "
+                "stream (nontemporal); memory-bound, no MFMA")
+    return (f"grouped schedule, {group} of {tiles} tiles per group: the group's c2v scratch ({group_mb:.0f} MB) is "
+            "meant to stay in the Infinity Cache between the phases, the v2c stream goes to HBM (nontemporal); "
+            "memory-bound, no MFMA")
 
 
 def find_traffic(kname):
@@ -343,7 +365,10 @@ def roofline(eng, G, st, cw_iters, coded=False, cpw=None) -> dict:
                                         "wave order over the row-block-major 604 MB group "
                                         "(profiles/r4/wrbench_rb_604MB.txt)")
     return {
-        "bound": "hbm", "kernel": names[dom], "bound_detail": bound_detail(eng, coded),
+        "bound": bound_label(eng), "kernel": names[dom], "bound_detail": bound_detail(eng, coded, E),
+        # the same kernels streaming every byte from HBM (bench.py main: the
+        # config3_hbm_streaming leg's frac, when that leg ran)
+        "frac_hbm_streaming": None,
         "ceiling_measured": ceiling,
         "ceiling_source": ceiling_src,
         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -428,10 +453,13 @@ def dna272(args, og, threads, max_iter=200):
     kp[...] = k8
     table = np.arange(-128, 128, dtype=np.float64) * synth.LLR_UNIT
     assert np.array_equal(table[k8.astype(np.int64) + 128], llr)
+    import dna_pipeline
+    first = dna_pipeline.gpu_decode_fn(G)  # the pipeline's first decode (decoder.py:553-562) from the codes
     G.decode_codes(k8, table, max_iter=max_iter, post=None)
     G.decode_codes(kp, table, max_iter=max_iter, post=None)
     G.decode(llr, max_iter=max_iter, post=None)
-    th, tp, tl = [], [], []
+    first.codes(k8, table, max_iter)
+    th, tp, tl, tf = [], [], [], []
     for _ in range(15):  # the host leg varies with the box's other tenants: median and min of 15 calls
         t = time.perf_counter()
         h2, _, it2, v2 = G.decode_codes(k8, table, max_iter=max_iter, post=None)
@@ -442,6 +470,10 @@ def dna272(args, og, threads, max_iter=200):
         t = time.perf_counter()
         h3, _, it3, v3 = G.decode(llr, max_iter=max_iter, post=None)
         tl.append(time.perf_counter() - t)
+        t = time.perf_counter()
+        h5 = first.codes(k8, table, max_iter)
+        tf.append(time.perf_counter() - t)
+    assert np.array_equal(h5, hard)
     assert np.array_equal(h2, hard) and np.array_equal(it2, it)
     assert np.array_equal(h3, hard) and np.array_equal(it3, it) and np.array_equal(v3, v2)
     assert np.array_equal(h4, hard) and np.array_equal(it4, it) and np.array_equal(v4, v2)
@@ -461,7 +493,12 @@ def dna272(args, og, threads, max_iter=200):
            "host_api_llr_ms_median": round(float(np.median(tl)) * 1e3, 3),
            "host_api_llr_ms_min": round(float(np.min(tl)) * 1e3, 3),
            "host_api_llr_includes": "Graph.decode -> ldpc_decode from the fp64 LLR matrix: host lattice check + "
-                                    "encode to int8 codes, then as above"}
+                                    "encode to int8 codes, then as above",
+           "pipeline_first_decode_ms_median": round(float(np.median(tf)) * 1e3, 3),
+           "pipeline_first_decode_ms_min": round(float(np.min(tf)) * 1e3, 3),
+           "pipeline_first_decode_includes": "dna_pipeline.gpu_decode_fn(G).codes: the first decode of "
+                                             "dna_pipeline.decode_trial when the LLR stage hands over its int8 codes "
+                                             "(dna_llr.LlrResult.codes) -- the host_api call above, from Python"}
     if og is not None:
         t = time.perf_counter()
         rh, _, rit, rv = og.decode_batch(llr, max_iter, threads=threads, want_post=False)
@@ -868,6 +905,10 @@ def main():
     threads = max(1, cpus["effective"] // max(1, local_world))
     if world == 1 and args.cpu_baseline:
         out["cpu_baseline"], (checked, bad, rows) = cpu_baseline(args, og, llr_fn, B, gpu_out, cpus)
+    elif world > 1 and args.cpu_baseline and rank == 0:
+        # rank 0's shard is checked by its cpu_baseline sample below (head,
+        # tail and interior rows), once
+        checked, bad, rows = 0, [], {}
     else:
         n = min(B, max(2, args.check_per_thread * threads))
         head = n - n // 2
@@ -885,9 +926,7 @@ def main():
             cb["while"] = f"ranks 1..{world - 1} idle in a gloo barrier after their own checks"
             cb["checked"], cb["mismatches"] = c_cb, len(bad_cb)
             out["cpu_baseline"] = cb
-            checked += c_cb
-            bad = bad + bad_cb
-            rows = dict(rows, cpu_baseline=rows_cb)
+            checked, bad, rows = c_cb, bad_cb, dict(rows_cb, via="cpu_baseline")
         grp.barrier()
     per = grp.gather({"rank": rank, "b0": b0, "B": B, "checked": checked, "mismatches": len(bad),
                       "first_mismatches": [b0 + k for k in bad[:4]], "threads": threads, "rows": rows})
@@ -933,6 +972,12 @@ def main():
         sec["config2_dna272"] = dna272(args, og, cpus["effective"])
         sec["config2_dna272"]["leg_wall_s"] = round(time.perf_counter() - t, 2)
         out["secondary"] = sec
+        hs = sec.get("config3_hbm_streaming")
+        if hs and out["roofline"]["bound"] != "hbm":
+            out["roofline"]["frac_hbm_streaming"] = hs["roofline"]["frac"]
+            out["roofline"]["frac_hbm_streaming_source"] = (
+                f"secondary.config3_hbm_streaming: the same check / variable kernels on {hs['batch']} codewords "
+                "in one grouped pass, every message byte from HBM")
         mismatches += sum(v.get("check", {}).get("mismatches", 0) for v in sec.values() if isinstance(v, dict))
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -46,10 +46,15 @@ __device__ __forceinline__ bool bit_is_zero(uint8_t c, bool hi)
     return c == 'A' || c == 'G';
 }
 
+// Every entry is k * L for an integer count difference k (decoder.py:297-314;
+// the +-2L / +-L special cases included), so the kernel can hand the decoder
+// its int8 codes directly (codes != nullptr): k saturated to [-127, 127], and
+// *overflow set (a plain store of 1) when some |k| > 127.
 __global__ void __launch_bounds__(256) k_dna_llr(const int32_t* __restrict__ kind, const int64_t* __restrict__ row_ptr,
                                                  const uint8_t* __restrict__ rows, const int32_t* __restrict__ row_q,
                                                  int32_t S, int32_t nt, double L, double* __restrict__ llr,
-                                                 uint8_t* __restrict__ int_mask)
+                                                 uint8_t* __restrict__ int_mask, int8_t* __restrict__ codes,
+                                                 int32_t* __restrict__ overflow)
 {
     const int32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     const int32_t k = blockIdx.y;  // nucleotide -> bits 2k, 2k+1
@@ -59,7 +64,7 @@ __global__ void __launch_bounds__(256) k_dna_llr(const int32_t* __restrict__ kin
     const int last_bit = 2 * nt - 1;
     for (int h = 0; h < 2; h++) {
         const int b = 2 * k + h;
-        double v = 0.0;
+        int n = 0;  // the count difference: the entry is n * L (0 for an int-0 entry)
         bool is_int = true;
         if (kd == 1) {
             int c0 = 0, c1 = 0, q0 = 0, q1 = 0;
@@ -70,15 +75,15 @@ __global__ void __launch_bounds__(256) k_dna_llr(const int32_t* __restrict__ kin
                 else { c1++; q1 += q; }
             }
             if (b == last_bit && c0 == 1 && c1 == 1) {
-                if (q0 < kQSkip && q1 >= kQHigh) { v = -2.0 * L; is_int = false; }
-                else if (q0 >= kQHigh && q1 < kQSkip) { v = 2.0 * L; is_int = false; }
+                if (q0 < kQSkip && q1 >= kQHigh) { n = -2; is_int = false; }
+                else if (q0 >= kQHigh && q1 < kQSkip) { n = 2; is_int = false; }
             } else {
-                v = (double)(c0 - c1) * L;
+                n = c0 - c1;
                 is_int = false;
             }
         } else if (kd == 2 && b == last_bit && r1 > r0) {
             if (row_q[r0] > kQHigh) {
-                v = bit_is_zero(rows[r0 * nt], false) ? L : -L;
+                n = bit_is_zero(rows[r0 * nt], false) ? 1 : -1;
                 is_int = false;
             }
         } else if (kd == 3 && b == last_bit) {
@@ -88,11 +93,17 @@ __global__ void __launch_bounds__(256) k_dna_llr(const int32_t* __restrict__ kin
                 if (bit_is_zero(rows[r * nt], false)) c0++;
                 else c1++;
             }
-            v = (double)(c0 - c1) * L;
+            n = c0 - c1;
             is_int = false;
         }
-        llr[(size_t)b * S + s] = v;
+        // (double)n * L: the reference's (count_0 - count_1) * math.log(...),
+        // and 2.0 * L, L, -L for the special cases -- the same doubles
+        llr[(size_t)b * S + s] = is_int ? 0.0 : (double)n * L;
         if (int_mask) int_mask[(size_t)b * S + s] = is_int;
+        if (codes) {
+            codes[(size_t)b * S + s] = (int8_t)max(-127, min(127, n));
+            if (n > 127 || n < -127) *overflow = 1;
+        }
     }
 }
 
@@ -153,17 +164,16 @@ int dev_copy_in(DevBuf& d, const void* src, size_t bytes)
 
 using ldpc::set_error;
 
-extern "C" {
-
-int ldpc_dna_llr(int32_t n_strands, const int32_t* kind, const int64_t* row_ptr, const uint8_t* rows,
-                 const int32_t* row_q, int32_t payload_nt, double llr_unit, double* llr, uint8_t* int_mask,
-                 int32_t device)
+static int dna_llr(int32_t n_strands, const int32_t* kind, const int64_t* row_ptr, const uint8_t* rows,
+                   const int32_t* row_q, int32_t payload_nt, double llr_unit, double* llr, uint8_t* int_mask,
+                   int8_t* codes, int32_t* codes_exact, int32_t device)
 {
     using namespace ldpc;
-    if (n_strands < 0 || payload_nt < 1 || !kind || !row_ptr || !llr) {
+    if (n_strands < 0 || payload_nt < 1 || !kind || !row_ptr || !llr || (codes && !codes_exact)) {
         set_error("ldpc_dna_llr: bad arguments");
         return LDPC_ERR_ARG;
     }
+    if (codes_exact) *codes_exact = 1;
     if (n_strands == 0) return LDPC_OK;
     const int64_t R = row_ptr[n_strands];
     if (R < 0 || row_ptr[0] != 0 || (R > 0 && (!rows || !row_q))) {
@@ -184,7 +194,7 @@ int ldpc_dna_llr(int32_t n_strands, const int32_t* kind, const int64_t* row_ptr,
     }
     LDPC_HIP(hipSetDevice(device));
     const size_t out_n = (size_t)2 * payload_nt * n_strands;
-    DevBuf dk, dp, dr, dq, dl, dm;
+    DevBuf dk, dp, dr, dq, dl, dm, dc, dov;
     int rc;
     if ((rc = dev_copy_in(dk, kind, sizeof(int32_t) * n_strands))) return rc;
     if ((rc = dev_copy_in(dp, row_ptr, sizeof(int64_t) * ((size_t)n_strands + 1)))) return rc;
@@ -192,14 +202,45 @@ int ldpc_dna_llr(int32_t n_strands, const int32_t* kind, const int64_t* row_ptr,
     if ((rc = dev_copy_in(dq, row_q, sizeof(int32_t) * (size_t)R))) return rc;
     LDPC_HIP(hipMalloc(&dl.p, sizeof(double) * out_n));
     if (int_mask) LDPC_HIP(hipMalloc(&dm.p, out_n));
+    if (codes) {
+        const int32_t zero = 0;
+        LDPC_HIP(hipMalloc(&dc.p, out_n));
+        if ((rc = dev_copy_in(dov, &zero, sizeof zero))) return rc;
+    }
     dim3 grid((unsigned)((n_strands + 255) / 256), (unsigned)payload_nt);
     hipLaunchKernelGGL(k_dna_llr, grid, dim3(256), 0, 0, dk.as<int32_t>(), dp.as<int64_t>(), dr.as<uint8_t>(),
                        dq.as<int32_t>(), n_strands, payload_nt, llr_unit, dl.as<double>(),
-                       int_mask ? dm.as<uint8_t>() : nullptr);
+                       int_mask ? dm.as<uint8_t>() : nullptr, codes ? dc.as<int8_t>() : nullptr,
+                       codes ? dov.as<int32_t>() : nullptr);
     LDPC_HIP(hipGetLastError());
     LDPC_HIP(hipMemcpy(llr, dl.p, sizeof(double) * out_n, hipMemcpyDeviceToHost));
     if (int_mask) LDPC_HIP(hipMemcpy(int_mask, dm.p, out_n, hipMemcpyDeviceToHost));
+    if (codes) {
+        int32_t ov = 0;
+        LDPC_HIP(hipMemcpy(codes, dc.p, out_n, hipMemcpyDeviceToHost));
+        LDPC_HIP(hipMemcpy(&ov, dov.p, sizeof ov, hipMemcpyDeviceToHost));
+        *codes_exact = ov ? 0 : 1;
+    }
     return LDPC_OK;
+}
+
+
+extern "C" {
+
+int ldpc_dna_llr(int32_t n_strands, const int32_t* kind, const int64_t* row_ptr, const uint8_t* rows,
+                 const int32_t* row_q, int32_t payload_nt, double llr_unit, double* llr, uint8_t* int_mask,
+                 int32_t device)
+{
+    return dna_llr(n_strands, kind, row_ptr, rows, row_q, payload_nt, llr_unit, llr, int_mask, nullptr, nullptr,
+                   device);
+}
+
+int ldpc_dna_llr_codes(int32_t n_strands, const int32_t* kind, const int64_t* row_ptr, const uint8_t* rows,
+                       const int32_t* row_q, int32_t payload_nt, double llr_unit, double* llr, uint8_t* int_mask,
+                       int8_t* codes, int32_t* codes_exact, int32_t device)
+{
+    return dna_llr(n_strands, kind, row_ptr, rows, row_q, payload_nt, llr_unit, llr, int_mask, codes, codes_exact,
+                   device);
 }
 
 int ldpc_dna_edit_distance(const uint8_t* seqs, const int64_t* offsets, const int32_t* lengths, int64_t n_seqs,

@@ -913,8 +913,23 @@ int Engine::sync()
 // member.  The host enqueues steps and stops kLag (1 for a single fill) polls
 // after the device reports an empty pool (occupied lanes == 0 once the claim
 // counter has passed B); the few surplus steps find no occupied lane.
+// A decode that stops on an error (a device fault at a poll, a step overrun)
+// leaves the steps it already enqueued running, and they can set the fault
+// words again.  Wait for them and clear the words, so that the error belongs
+// to this decode alone: the next sync or decode on the engine starts clean.
 int Engine::run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
                      int post_kind, int32_t* d_iters, uint8_t* d_valid)
+{
+    const int rc = run_cont_steps(d_in, in_kind, B, max_iter, d_hard, d_post, post_kind, d_iters, d_valid);
+    if (rc != LDPC_OK && h_fault && hipStreamSynchronize(stream) == hipSuccess) {
+        volatile unsigned long long* w = h_fault;
+        for (int k = 1; k < dev::kFaultWords; k++) w[k] = 0ull;
+    }
+    return rc;
+}
+
+int Engine::run_cont_steps(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard,
+                           double* d_post, int post_kind, int32_t* d_iters, uint8_t* d_valid)
 {
     using namespace dev;
     const int msa = algo == LDPC_ALGO_MSA;

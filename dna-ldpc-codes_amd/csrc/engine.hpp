@@ -134,8 +134,12 @@ struct Engine {
     // resolve_schedule already returned (the host API's slots)
     int init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, const ldpc_schedule* schedule,
              bool resolved = false);
+    // continuous batching; on an error the queued steps are drained and the
+    // fault words cleared before returning (each fault is reported once)
     int run_cont(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
                  int post_kind, int32_t* d_iters, uint8_t* d_valid);
+    int run_cont_steps(const double* d_in, int in_kind, int64_t B, int32_t max_iter, uint8_t* d_hard, double* d_post,
+                       int post_kind, int32_t* d_iters, uint8_t* d_valid);
     // decode Bc <= cap codewords whose [Bc][N] input is at d_in (device)
     int run_chunk(const double* d_in, int in_kind, int64_t Bc, int32_t max_iter, uint8_t* d_hard, double* d_post,
                   int post_kind, int32_t* d_iters, uint8_t* d_valid);

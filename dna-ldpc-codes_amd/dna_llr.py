@@ -86,6 +86,15 @@ class LlrResult:
     n_pairs: int = 0               # edit-distance pairs evaluated on the GPU
     n_aligned_strands: int = 0
     erased: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))  # strands with no LLRs
+    # the count differences: llr == codes * unit exactly (decoder.py:297-314);
+    # None when some |count difference| > 127 (no int8 code)
+    codes: Optional[np.ndarray] = None  # [2*PAYLOAD_NT][S] int8
+    unit: float = 0.0                   # ln((1-eps)/eps)
+
+    def code_table(self) -> np.ndarray:
+        """table[k + 128] = k * unit: with `codes`, the input of
+        Graph.decode_codes (the same doubles as llr)."""
+        return np.arange(-128, 128, dtype=np.float64) * self.unit
 
     def write_soft_files(self, directory: str, rs: int):
         """soft<rs>_n18432_m1860_<i>.txt, i = 1..272 (decoder.py:511-516)."""
@@ -103,6 +112,7 @@ def _lib():
     if not getattr(L, "_dna_bound", False):
         vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
         L.ldpc_dna_llr.argtypes = [i32, vp, vp, vp, vp, i32, C.c_double, vp, vp, i32]
+        L.ldpc_dna_llr_codes.argtypes = [i32, vp, vp, vp, vp, i32, C.c_double, vp, vp, vp, vp, i32]
         L.ldpc_dna_edit_distance.argtypes = [vp, vp, vp, i64, vp, vp, i64, vp, i32]
         L.ldpc_write_soft_files.argtypes = [C.c_char_p, i32, vp, vp, i32, i32]
         L.ldpc_py_float_repr.argtypes = [C.c_double, C.c_char_p, i32]
@@ -288,8 +298,10 @@ def build_llr(index_vals: Sequence[int], seqs: Sequence[str], quals: Sequence[in
     unit = math.log((1 - eps) / eps)  # decoder.py:297
     llr = np.zeros((2 * PAYLOAD_NT, S), np.float64)
     mask = np.zeros((2 * PAYLOAD_NT, S), np.uint8)
-    mod._check(L.ldpc_dna_llr(S, _p(plan.kind), _p(plan.row_ptr), _p(plan.rows), _p(plan.row_q), PAYLOAD_NT,
-                              unit, _p(llr), _p(mask), device))
+    codes = np.zeros((2 * PAYLOAD_NT, S), np.int8)
+    exact = C.c_int32(0)
+    mod._check(L.ldpc_dna_llr_codes(S, _p(plan.kind), _p(plan.row_ptr), _p(plan.rows), _p(plan.row_q), PAYLOAD_NT,
+                                    unit, _p(llr), _p(mask), _p(codes), C.byref(exact), device))
     return LlrResult(llr=llr, int_mask=mask, kind=plan.kind, n_reads_valid=plan.n_reads_valid,
                      n_pairs=plan.n_pairs, n_aligned_strands=plan.n_aligned_strands,
-                     erased=np.nonzero(plan.kind == KIND_NONE)[0])
+                     erased=np.nonzero(plan.kind == KIND_NONE)[0], codes=codes if exact.value else None, unit=unit)

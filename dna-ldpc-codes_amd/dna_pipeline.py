@@ -18,6 +18,14 @@ the 272+ `ldpc.exe` processes and soft/dec text files:
 
 All decodes of one stage go to the GPU in ONE batched call.  `decode_fn` is
 injectable so tests can run the identical flow on the CPU oracle.
+
+The first decode's LLRs are count differences times ln((1-eps)/eps)
+(decoder.py:314): when the caller has them as int8 codes (dna_llr's
+LlrResult.codes, made by the LLR kernel itself), the GPU decode_fn takes the
+codes and the 256-entry table k * unit (Graph.decode_codes) -- the same
+doubles, without the host lattice pass over the fp64 matrix that the fp64
+entry needs.  The second decode's rescaled LLRs are off that lattice and keep
+the fp64 entry.
 """
 from __future__ import annotations
 
@@ -28,6 +36,13 @@ from typing import Callable, Dict, List, Optional
 import numpy as np
 
 DecodeFn = Callable[[np.ndarray, int], np.ndarray]  # (llr [B][N], max_iter) -> hard [B][N]
+# optional attribute `codes` of a DecodeFn: (codes int8 [B][N], table [256], max_iter) -> hard [B][N],
+# the decode of llr = table[codes + 128]
+
+
+def code_table(unit: float) -> np.ndarray:
+    """table[k + 128] = k * unit: the doubles (count_0 - count_1) * unit of decoder.py:314."""
+    return np.arange(-128, 128, dtype=np.float64) * unit
 
 
 def gpu_decode_fn(graph=None, algo="bp") -> DecodeFn:
@@ -38,6 +53,11 @@ def gpu_decode_fn(graph=None, algo="bp") -> DecodeFn:
         hard, _, _, _ = g.decode(llr, max_iter=max_iter, algo=algo, post=None)
         return hard
 
+    def codes(k: np.ndarray, table: np.ndarray, max_iter: int) -> np.ndarray:
+        hard, _, _, _ = g.decode_codes(k, table, max_iter=max_iter, algo=algo, post=None)
+        return hard
+
+    fn.codes = codes
     return fn
 
 
@@ -49,14 +69,24 @@ def rescale(llr: np.ndarray, eps: float, eps2: float) -> np.ndarray:
 
 
 def decode_trial(llr: np.ndarray, codewords: np.ndarray, eps: float = 0.02, max_iter: int = 200,
-                 decode_fn: Optional[DecodeFn] = None, faithful: bool = True) -> Dict:
+                 decode_fn: Optional[DecodeFn] = None, faithful: bool = True,
+                 codes: Optional[np.ndarray] = None) -> Dict:
     """Run the LDPC part of one decoder.py trial.  llr: [n_cw][N] (row i = soft
-    file i+1), codewords: [n_cw][N] true codewords (the genie)."""
+    file i+1), codewords: [n_cw][N] true codewords (the genie).  codes
+    (optional, int8 [n_cw][N]): the count differences with llr == codes *
+    ln((1-eps)/eps) exactly, as the producer guarantees (dna_llr.build_llr);
+    a decode_fn with a `codes` attribute then decodes them for the first
+    decode."""
     decode_fn = decode_fn or gpu_decode_fn()
     llr = np.ascontiguousarray(llr, dtype=np.float64)
     n_cw, N = llr.shape
     t0 = time.perf_counter()
-    hard = decode_fn(llr, max_iter)
+    if codes is not None and hasattr(decode_fn, "codes"):
+        if codes.shape != llr.shape or codes.dtype != np.int8:
+            raise ValueError("codes must be int8 with the shape of llr")
+        hard = decode_fn.codes(codes, code_table(math.log((1 - eps) / eps)), max_iter)
+    else:
+        hard = decode_fn(llr, max_iter)
     t_first = time.perf_counter() - t0
     errors = (hard != codewords).sum(axis=1)
     fail = [i + 1 for i in range(n_cw) if errors[i] != 0]
@@ -102,7 +132,8 @@ def trial_from_reads(reads, codewords: np.ndarray, eps: float = 0.02, max_iter: 
     t0 = time.perf_counter()
     built = dna_llr.build_llr(*reads, eps=eps, align_fn=align_fn, device=device)
     t_llr = time.perf_counter() - t0
-    res = decode_trial(built.llr, codewords, eps=eps, max_iter=max_iter, decode_fn=decode_fn, faithful=faithful)
+    res = decode_trial(built.llr, codewords, eps=eps, max_iter=max_iter, decode_fn=decode_fn, faithful=faithful,
+                       codes=built.codes)
     res.update(t_llr_s=t_llr, n_erased_strands=int(len(built.erased)), n_reads_valid=built.n_reads_valid,
                llr=built)
     return res

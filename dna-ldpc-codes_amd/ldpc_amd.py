@@ -135,7 +135,7 @@ EXPORTS = [
     "ldpc_decode_codes",
     "ldpc_engine_create", "ldpc_engine_create_ex", "ldpc_engine_info", "ldpc_engine_free", "ldpc_engine_decode", "ldpc_engine_sync", "ldpc_engine_stream",
     "ldpc_engine_decode_codes", "ldpc_engine_gen_bsc", "ldpc_engine_gen_bsc_codes", "ldpc_engine_set_params", "ldpc_engine_profile", "ldpc_engine_stats", "ldpc_dev_malloc", "ldpc_dev_free",
-    "ldpc_dev_memcpy", "ldpc_host_alloc", "ldpc_host_free", "ldpc_dna_llr", "ldpc_dna_edit_distance", "ldpc_write_soft_files", "ldpc_py_float_repr",
+    "ldpc_dev_memcpy", "ldpc_host_alloc", "ldpc_host_free", "ldpc_dna_llr", "ldpc_dna_llr_codes", "ldpc_dna_edit_distance", "ldpc_write_soft_files", "ldpc_py_float_repr",
 ]
 
 

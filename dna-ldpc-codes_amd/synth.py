@@ -38,10 +38,26 @@ def load_codewords() -> np.ndarray:
 def dna_like_llrs(codewords: np.ndarray, seed: int = 0, reads: int = 72000, sub: float = 0.01,
                   eps: float = EPSILON) -> np.ndarray:
     """LLRs [n_cw][N] for the DNA batch (see module doc)."""
+    k = dna_like_counts(codewords, seed=seed, reads=reads, sub=sub)
+    unit = math.log((1 - eps) / eps)
+    llr = k.astype(np.float64) * unit  # int * double, as (count_0-count_1)*math.log(...)
+    return np.ascontiguousarray(llr)
+
+
+def dna_like_codes(codewords: np.ndarray, seed: int = 0, reads: int = 72000, sub: float = 0.01) -> np.ndarray:
+    """The count differences of dna_like_llrs as int8 codes (dna_like_llrs ==
+    codes * ln((1-eps)/eps)); ValueError if one does not fit."""
+    k = dna_like_counts(codewords, seed=seed, reads=reads, sub=sub)
+    if k.size and np.abs(k).max() > 127:
+        raise ValueError("a count difference exceeds the int8 code range")
+    return np.ascontiguousarray(k.astype(np.int8))
+
+
+def dna_like_counts(codewords: np.ndarray, seed: int = 0, reads: int = 72000, sub: float = 0.01) -> np.ndarray:
+    """Count differences count_0 - count_1 [n_cw][N] (int64) of the DNA batch."""
     n_cw, N = codewords.shape
     if n_cw % 2:
         raise ValueError("codewords come in nucleotide pairs (bits 2k, 2k+1 of a strand)")
-    unit = math.log((1 - eps) / eps)
     rng = np.random.default_rng(seed)
     # strand j: nucleotides k = 0..n_cw/2-1, base = 2*bit(2k) + bit(2k+1)
     bits = codewords.T.astype(np.int64)  # [N][n_cw]
@@ -57,9 +73,7 @@ def dna_like_llrs(codewords: np.ndarray, seed: int = 0, reads: int = 72000, sub:
     ones = np.zeros((N, n_cw), np.int64)
     np.add.at(ones, strand, rbits)
     zeros = nreads[:, None] - ones
-    k = (zeros - ones).T  # [n_cw][N] count difference
-    llr = k.astype(np.float64) * unit  # int * double, as (count_0-count_1)*math.log(...)
-    return np.ascontiguousarray(llr)
+    return np.ascontiguousarray((zeros - ones).T)  # [n_cw][N] count difference
 
 
 # --- counter-based BSC generator (bit-identical to kernels.hpp k_gen_bsc) ---

@@ -341,6 +341,16 @@ int ldpc_dna_llr(int32_t n_strands, const int32_t *kind, const int64_t *row_ptr,
                  const int32_t *row_q, int32_t payload_nt, double llr_unit, double *llr, uint8_t *int_mask,
                  int32_t device);
 
+/* ldpc_dna_llr, plus each entry's count difference as an int8 code:
+ * llr = codes * llr_unit exactly (decoder.py:297-314), codes
+ * [2*payload_nt][n_strands].  *codes_exact = 1 when every |code| <= 127,
+ * else 0 (the codes are then saturated and only llr is usable).  The codes
+ * and the table k * llr_unit feed ldpc_decode_codes / the engine's coded
+ * input without a host lattice pass over the fp64 matrix. */
+int ldpc_dna_llr_codes(int32_t n_strands, const int32_t *kind, const int64_t *row_ptr, const uint8_t *rows,
+                       const int32_t *row_q, int32_t payload_nt, double llr_unit, double *llr, uint8_t *int_mask,
+                       int8_t *codes, int32_t *codes_exact, int32_t device);
+
 /* Levenshtein distances of sequence pairs on `device`
  * (def_func.edit_dist, def_func.py:10-26).  Sequence i is
  * seqs[offsets[i] .. offsets[i]+lengths[i]); lengths <= 800. */

@@ -93,3 +93,38 @@ def test_config4_leg_selection():
     assert [b.config4_total("auto", n, 0) for n in (1, 2, 4)] == [0, 0, 0]
     assert b.config4_total("4096", 2, 0) == 4096 and b.config4_total("4096", 1, 0) == 0
     assert b.config4_total("0", 8, 0) == 0
+
+
+def test_roofline_bound_names_residency():
+    """The headline's resident pool lives in the 256 MB Infinity Cache: its
+    roofline says so in `bound`, and carries the HBM-streaming fraction of the
+    same kernels beside `frac` (filled by main() from the
+    config3_hbm_streaming leg)."""
+    b = _bench()
+    G = types.SimpleNamespace(N=18432, M=2048, E=147456)
+    st = {"check": {"ms": 0.07, "sampled": 1, "launches": 100}, "variable": {"ms": 0.068, "sampled": 1, "launches": 100},
+          "syndrome": {"ms": 0.0, "sampled": 0, "launches": 0}}
+    r = b.roofline(_eng(), G, st, 100 * 192.0, coded=True)
+    assert r["bound"] == "hbm+mall (resident pool)"
+    assert "frac_hbm_streaming" in r and r["frac"] > 0
+    g = b.roofline(_eng(resident=False, cap=16384, group_tiles=-1), G, st, 100 * 192.0)
+    assert g["bound"] == "hbm" and "frac_hbm_streaming" in g
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'out["roofline"]["frac_hbm_streaming"] = hs["roofline"]["frac"]' in src
+
+
+def test_bound_detail_grouped_schedules():
+    """_bound_detail tells a one-pass grouped run (every tile in one group)
+    from a multi-pass one, with the working set from the graph's E
+    (ADVICE r5)."""
+    b = _bench()
+    E = 147456
+    one = b._bound_detail(_eng(resident=False, cap=16384, group_tiles=-1), E)
+    assert one.startswith("one grouped pass over every tile (256)") and "streams from HBM" in one
+    assert b._bound_detail(_eng(resident=False, cap=16384, group_tiles=256), E).startswith("one grouped pass")
+    multi = b._bound_detail(_eng(resident=False, cap=16384, group_tiles=4), E)
+    assert multi.startswith("grouped schedule, 4 of 256 tiles per group") and "exceeds" in multi  # 288 MB
+    small = b._bound_detail(_eng(resident=False, cap=16384, group_tiles=2), E)
+    assert "meant to stay in the Infinity Cache" in small  # 144 MB
+    tiny = b._bound_detail(_eng(resident=False, cap=16384, group_tiles=2), 1000)
+    assert "(1 MB)" in tiny

@@ -67,6 +67,9 @@ def test_build_llr_bitexact_vs_oracle(gpu, dorc, codewords, tmp_path, case):
     llr, mask = _oracle_arrays(by_strand)
     assert np.array_equal(res.llr.view(np.uint64), llr.view(np.uint64))
     assert np.array_equal(res.int_mask, mask)
+    # the kernel's int8 codes give back every LLR bit for bit through the table k * ln49
+    assert res.codes is not None
+    assert np.array_equal(res.code_table()[res.codes.astype(np.int64) + 128].view(np.uint64), llr.view(np.uint64))
     # every strand kind occurs
     assert set(np.unique(res.kind).tolist()) == {0, 1, 2, 3}
     assert res.n_pairs > 0 and res.n_aligned_strands > 0
@@ -93,7 +96,10 @@ def test_full_scale_reads_decode(gpu, codewords):
     built = res["llr"]
     assert built.llr.shape == (272, 18432)
     assert res["first_success"] == 272 and not res["fail_second"]
-    # the count rule: LLR / ln49 is an integer count difference everywhere
+    # the count rule: LLR / ln49 is an integer count difference everywhere,
+    # and the kernel's int8 codes are those differences (the first decode's input)
     k = built.llr / math.log(49.0)
     assert np.array_equal(k, np.rint(k))
+    assert built.codes is not None and built.codes.dtype == np.int8
+    assert np.array_equal(built.code_table()[built.codes.astype(np.int64) + 128], built.llr)
     assert 0 < res["n_erased_strands"] < 18432 * 0.05
