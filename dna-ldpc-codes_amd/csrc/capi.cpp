@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdint>
 #include <cstdio>
 #include <cmath>
 #include <condition_variable>
@@ -35,6 +36,8 @@ using ldpc::set_error;
 // shards up to this many codewords get a lane pool holding all of them
 // (the 272-codeword DNA batch: 248k cw/s grouped vs 194k through the
 // resident pool); larger ones use the engine's own pool
+constexpr int kMaxDevices = 64;       // opts.n_devices bound (one host thread per device)
+constexpr int kMaxHostThreads = 256;  // opts.host_threads clamp
 constexpr int64_t kExplicitPoolMax = 1024;
 constexpr int64_t kXferChunk = 4096;  // codewords per PCIe chunk (at least); shards of <= kExplicitPoolMax
                                       // cross in one chunk (A/B on the DNA batch: chunks of 128 or 192
@@ -480,13 +483,28 @@ static int host_decode(const ldpc_graph* gc, const HostInput& in, int64_t B, int
         set_error("LDPC_POST_RATIO is BP-only");
         return LDPC_ERR_ARG;
     }
+    // B [B][N] fp64 values must be addressable (the host code forms B * N * 8)
+    if (B > (int64_t)(PTRDIFF_MAX / 8) / (int64_t)std::max<int32_t>(1, g->h.N)) {
+        set_error("batch too large: B * N * 8 bytes overflow the address space");
+        return LDPC_ERR_ARG;
+    }
+    if (o.n_devices > kMaxDevices) {
+        set_error("opts.n_devices above " + std::to_string(kMaxDevices));
+        return LDPC_ERR_ARG;
+    }
     if (B == 0) return LDPC_OK;
 
     std::vector<int> devs;
     const int ndev = std::max(1, (int)o.n_devices);
-    for (int i = 0; i < ndev; i++) devs.push_back(o.devices ? o.devices[i] : i);
+    for (int i = 0; i < ndev; i++) {
+        devs.push_back(o.devices ? o.devices[i] : i);
+        if (devs.back() < 0) { set_error("negative device ordinal"); return LDPC_ERR_ARG; }
+    }
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-    const int host_threads = o.host_threads > 0 ? o.host_threads : std::min(16, std::max(1, hw / ndev));
+    // host threads for exp / packing: the caller's count, clamped (each is an
+    // OS thread of this call's worker pool)
+    const int host_threads = o.host_threads > 0 ? std::min(o.host_threads, kMaxHostThreads)
+                                                : std::min(16, std::max(1, hw / ndev));
     const ldpc_schedule sched = ldpc::resolve_schedule(o.schedule);
     const bool lr_table = ldpc::sched_flag(sched, LDPC_SCHED_LR_TABLE);
     // the only environment variable the library reads: a debug print of the

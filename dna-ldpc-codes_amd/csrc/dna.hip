@@ -176,7 +176,7 @@ static int dna_llr(int32_t n_strands, const int32_t* kind, const int64_t* row_pt
     if (codes_exact) *codes_exact = 1;
     if (n_strands == 0) return LDPC_OK;
     const int64_t R = row_ptr[n_strands];
-    if (R < 0 || row_ptr[0] != 0 || (R > 0 && (!rows || !row_q))) {
+    if (R < 0 || R > INT64_MAX / payload_nt || row_ptr[0] != 0 || (R > 0 && (!rows || !row_q))) {
         set_error("ldpc_dna_llr: bad row_ptr / rows");
         return LDPC_ERR_ARG;
     }
@@ -257,8 +257,8 @@ int ldpc_dna_edit_distance(const uint8_t* seqs, const int64_t* offsets, const in
     int64_t total = 0;
     int32_t max_len = 0;
     for (int64_t i = 0; i < n_seqs; i++) {
-        if (lengths[i] < 0 || offsets[i] < 0) {
-            set_error("ldpc_dna_edit_distance: negative length/offset");
+        if (lengths[i] < 0 || offsets[i] < 0 || offsets[i] > INT64_MAX - lengths[i]) {
+            set_error("ldpc_dna_edit_distance: negative or overflowing length/offset");
             return LDPC_ERR_ARG;
         }
         total = std::max<int64_t>(total, offsets[i] + lengths[i]);

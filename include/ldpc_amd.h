@@ -121,8 +121,8 @@ typedef struct ldpc_schedule {
 } ldpc_schedule;
 
 typedef struct ldpc_opts {
-    int32_t n_devices;      /* <= 0: use device 0 only */
-    const int32_t *devices; /* device ordinals (NULL: 0..n_devices-1) */
+    int32_t n_devices;      /* <= 0: use device 0 only; at most 64 (else LDPC_ERR_ARG) */
+    const int32_t *devices; /* device ordinals >= 0 (NULL: 0..n_devices-1) */
     int64_t chunk;          /* lane pool: codewords resident per device at once (0: auto --
                                all of a shard of <= 1024, else the engine's own pool);
                                codewords cross PCIe in double-buffered chunks of
@@ -130,7 +130,7 @@ typedef struct ldpc_opts {
     int32_t exp_on_host;    /* BP: compute LR = exp(LLR) with the host libm, exactly as
                                DNA_main.cpp:1344 does (default 1 when opts == NULL) */
     int32_t post_kind;      /* LDPC_POST_* */
-    int32_t host_threads;   /* threads for host exp/packing (0: auto) */
+    int32_t host_threads;   /* threads for host exp/packing (0: auto; clamped to 256) */
     int32_t msa_precision;  /* LDPC_ALGO_QMSA: message bits q, 2..16 (Set_MSA dec.cpp:1683) */
     int32_t msa_offset;     /* LDPC_ALGO_QMSA: offset beta (1 = offset min-sum, decoder_type 21) */
     int32_t reserved0;

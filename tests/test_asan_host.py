@@ -271,6 +271,27 @@ def test_oracle_decode_sanitized(hc, algo, p):
         assert "valid=1" in out[0] and "ones=0 syndrome=0" in out[0]
 
 
+@pytest.mark.timeout(900)
+def test_c_abi_sanitized(tmp_path):
+    """The whole C ABI with its host code under ASan + UBSan
+    (tests/asan/abi_check.cpp over build/libldpc_amd_asan.so): null pointers,
+    negative / oversized counts, bad enums, malformed files, and decodes with
+    good arguments that reach the (absent) device -- every call returns its
+    status, no sanitizer report.  Regression: opts.host_threads = 2^30 made
+    the host decode start ~28k threads before this round's clamp, and
+    opts.n_devices / B * N / an edit-distance offset near INT64_MAX were
+    unchecked."""
+    if not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("no hipcc")
+    subprocess.run(["make", "-s", "-j", "8", "-C", ASAN_DIR, "abi"], check=True, capture_output=True, timeout=900)
+    env = dict(os.environ, **SAN_ENV)
+    r = subprocess.run([os.path.join(ASAN_DIR, "build", "abi_check"), PCHK, str(tmp_path)], capture_output=True,
+                       text=True, env=env, timeout=300)
+    assert "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-2000:])
+    assert r.stdout.strip().startswith("ok abi ") and "MISMATCH" not in r.stdout
+
+
 def test_cli_refuses_bad_inputs(tmp_path):
     """bin/ldpc exits 1 with a message before any decode (no GPU needed)."""
     if not os.access(CLI, os.X_OK):
