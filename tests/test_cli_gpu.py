@@ -167,3 +167,30 @@ def test_cli_puncturing_shortening(tmp_path, og, codewords):
     txt = open(res).read()
     assert "[Type: 2] Punctuation_VN:10~20 \n\n" in txt
     assert "code rate     : %.3f\n" % (1.0 - (2048 - 33) / (18432 - 33)) in txt
+
+
+@pytest.mark.parametrize("algo,dtype", [("bp", 0), ("msa", 20)])
+def test_cli_nonfinite_tokens(tmp_path, og, codewords, algo, dtype):
+    """Soft-file tokens fscanf("%lf") accepts and Python's str() writes for
+    non-finite floats -- nan, inf, -inf -- plus an exponent form and a hex
+    float: the CLI reads them (cli_io.cpp, strtod) and decodes what the oracle
+    decodes on the same values (the NaN / overflow guards of dec.cpp:676-687
+    on the device)."""
+    d = str(tmp_path)
+    llr = synth.bsc_llrs(codewords, 0, 1, seed=11, p=0.002)[0].copy()
+    toks = [str(float(v)) for v in llr]
+    for j, t in ((5, "nan"), (77, "inf"), (901, "-inf"), (4000, "1e-300"), (4001, "0x1.8p1"), (9000, "-0.0")):
+        toks[j] = t
+        llr[j] = float.fromhex(t) if t.startswith("0x") else float(t)
+    cwb, soft = f"codeword_n18432_m1860_3", f"soft72000_n18432_m1860_3"
+    with open(os.path.join(d, cwb + ".txt"), "w") as f:
+        f.write("".join(f"{int(b)} " for b in codewords[0]))
+    with open(os.path.join(d, soft + ".txt"), "w") as f:
+        f.write(" ".join(toks) + "\n")
+    shutil.copyfile(PCHK, os.path.join(d, "decode_n18432_m2048_final.pchk"))
+    argv = [EXE, "0", str(dtype), "0", "7", "40", "1", cwb, soft, "decode_n18432_m2048_final", "0", "0", "0", "0"]
+    r = subprocess.run(argv, cwd=d, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    dec = np.array(open(os.path.join(d, f"dec_{cwb}.txt")).read().split(), dtype=np.uint8)
+    h, _, _, _ = og.decode_batch(llr[None, :], 40, algo=0 if algo == "bp" else 1, threads=1, want_post=False)
+    assert np.array_equal(dec, h[0])
