@@ -1,7 +1,6 @@
 // cli_io.cpp -- see cli_io.hpp.
 #include "cli_io.hpp"
 
-#include <cerrno>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -44,8 +43,7 @@ bool parse_int(const std::string& tok, int* v)
     if (p >= tok.size()) return false;
     for (size_t i = p; i < tok.size(); i++)
         if (tok[i] < '0' || tok[i] > '9') return false;
-    errno = 0;
-    const long x = std::strtol(tok.c_str(), nullptr, 10);
+    const long x = std::strtol(tok.c_str(), nullptr, 10);  // LONG_MIN / LONG_MAX out of range
     *v = x > INT_MAX ? INT_MAX : x < INT_MIN ? INT_MIN : (int)x;
     return true;
 }
