@@ -31,7 +31,9 @@ def test_bench_bsc_line(gpu, algo, p):
                  "--cpu-seconds", "1", "--secondary", "0")
     assert out["steps"] == 1 and out["dtype"] == "f64"
     rl = out["roofline"]
-    assert rl["bound"] == "hbm" and rl["unit"] == "GB/s" and rl["peak"] == 8000.0
+    # BP's default schedule is the resident pool, sized to the Infinity Cache (MALL)
+    assert rl["bound"] == ("hbm+mall (resident pool)" if algo == "bp" else "hbm")
+    assert rl["unit"] == "GB/s" and rl["peak"] == 8000.0 and "frac_hbm_streaming" in rl
     assert rl["achieved"] > 0 and 0 < rl["frac"] < 1.2
     cb = out["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["per_core"] > 0
@@ -65,6 +67,11 @@ def test_bench_secondary_legs(gpu):
     assert h["check"]["mismatches"] == 0 and h["check"]["checked"] == 16 and h["roofline"]["achieved"] > 0
     assert h["roofline"]["kernel"].startswith("k_check_bp<72,true,false>") or \
         h["roofline"]["kernel"].startswith("k_var_m<false,8,true,true")
+    # the headline states both fractions: its resident pool's and the HBM-streaming leg's
+    assert h["roofline"]["bound"] == "hbm" and out["roofline"]["bound"] == "hbm+mall (resident pool)"
+    assert out["roofline"]["frac_hbm_streaming"] == h["roofline"]["frac"]
+    # the pipeline's first decode from the LLR stage's int8 codes
+    assert d["pipeline_first_decode_ms_median"] > 0
 
 
 def test_bench_dna272_line(gpu):
