@@ -1,8 +1,8 @@
 """Race detection on the C ABI's host side, on an
 MI355X: tests/tsan/build/tsan_check over a ThreadSanitizer build of the
 library's host code (tests/tsan/Makefile; built on the CPU by
-__graft_entry__.build()).  Six threads share one graph -- BP and min-sum
-host decodes, coded input, the device-resident engine, graph loads and
+__graft_entry__.build()).  Eight threads share one graph -- BP and min-sum
+host decodes (two of them over two PCIe chunks), coded input, the device-resident engine, graph loads and
 per-thread errors -- plus a two-shard call's per-device worker threads;
 results must equal the single-thread calls and ThreadSanitizer must report
 nothing.  Uninstrumented libraries (the HIP runtime) are ignored

@@ -5,13 +5,15 @@
 // code as usual -- and run on an MI355X by tests/test_tsan_gpu.py.
 //
 // The threading contract (include/ldpc_amd.h): a graph is
-// shareable, calls are reentrant, errors are per thread.  Six threads at once,
-// two rounds each, on ONE graph:
+// shareable, calls are reentrant, errors are per thread.  Eight threads at
+// once, two rounds each, on ONE graph:
 //   0, 1  ldpc_decode BP (host exp; one with posteriors), different batches
 //   2     ldpc_decode min-sum
 //   3     ldpc_decode_codes (int8 codes + table)
-//   4     the device-resident engine: create, gen_bsc on device, decode, sync
-//   5     graph loads that fail and succeed, host syndromes, error strings
+//   4, 5  4160 codewords each (BP fp64, min-sum codes): two PCIe chunks, so
+//         the helper thread that prepares the next chunk runs too
+//   6     the device-resident engine: create, gen_bsc on device, decode, sync
+//   7     graph loads that fail and succeed, host syndromes, error strings
 // plus one call with two shards on device 0 (the per-device worker threads).
 // Every decode result must equal the same call made alone first.  A race is
 // a ThreadSanitizer report (the test fails on it); a wrong result prints
@@ -163,15 +165,20 @@ int main(int argc, char** argv)
     ldpc_graph_info(g, &M32, &N32, &E, nullptr, nullptr, nullptr, nullptr);
     const int64_t N = N32;
 
-    std::vector<Job> jobs(4);
+    // jobs 4 and 5 span two PCIe chunks (> 4096 codewords): the helper thread
+    // that prepares chunk c + 1 while chunk c decodes
+    const int NJ = 6;
+    std::vector<Job> jobs(NJ);
     jobs[0] = {0, LDPC_ALGO_BP, 64, 20, true, bsc(64, N, 0.004, 1), {}};
     jobs[1] = {0, LDPC_ALGO_BP, 130, 30, false, bsc(130, N, 0.02, 2), {}};
     jobs[2] = {0, LDPC_ALGO_MSA, 80, 25, true, bsc(80, N, 0.002, 3), {}};
     jobs[3] = {1, LDPC_ALGO_BP, 96, 20, false, {}, {}};
-    {
-        const std::vector<double> x = bsc(96, N, 0.003, 4);
-        jobs[3].codes.resize(x.size());
-        for (size_t i = 0; i < x.size(); i++) jobs[3].codes[i] = x[i] > 0 ? 1 : -1;
+    jobs[4] = {0, LDPC_ALGO_BP, 4160, 3, false, bsc(4160, N, 0.01, 5), {}};
+    jobs[5] = {1, LDPC_ALGO_MSA, 4160, 3, false, {}, {}};
+    for (int j : {3, 5}) {
+        const std::vector<double> x = bsc(jobs[(size_t)j].B, N, 0.003, 4 + (uint64_t)j);
+        jobs[(size_t)j].codes.resize(x.size());
+        for (size_t i = 0; i < x.size(); i++) jobs[(size_t)j].codes[i] = x[i] > 0 ? 1 : -1;
     }
     // alone first
     std::vector<Out> alone;
@@ -179,12 +186,12 @@ int main(int argc, char** argv)
     const Out eng_alone = engine_run(g, 70, N, 15);
 
     std::vector<std::thread> th;
-    for (int t = 0; t < 6; t++)
+    for (int t = 0; t < NJ + 2; t++)
         th.emplace_back([&, t] {
             for (int rep = 0; rep < 2; rep++) {
-                if (t < 4) {
+                if (t < NJ) {
                     if (!(run(g, jobs[(size_t)t], N) == alone[(size_t)t])) fail("thread " + std::to_string(t));
-                } else if (t == 4) {
+                } else if (t == NJ) {
                     if (!(engine_run(g, 70, N, 15) == eng_alone)) fail("engine thread");
                 } else {
                     int e2 = 0;
@@ -210,6 +217,6 @@ int main(int argc, char** argv)
     if (!(run(g, jobs[1], N, &o) == alone[1])) fail("two shards on device 0");
 
     ldpc_graph_free(g);
-    std::printf("ok tsan: 6 threads x 2 rounds + a two-shard call, results equal the single-thread calls\n");
+    std::printf("ok tsan: 8 threads x 2 rounds + a two-shard call, results equal the single-thread calls\n");
     return g_bad ? 3 : 0;
 }
