@@ -240,7 +240,9 @@ int ldpc_decode_codes(const ldpc_graph *g, const int8_t *codes, const double *ta
 typedef struct ldpc_engine ldpc_engine;
 
 /* One engine = one device + one HIP stream + chunk-sized message buffers,
- * with the default schedule. */
+ * with the default schedule.  An engine serves one thread at a time (its
+ * calls enqueue on its one stream); engines on one graph may run in
+ * different threads at once. */
 ldpc_engine *ldpc_engine_create(const ldpc_graph *g, int32_t device, int32_t algo, int64_t chunk, int *err);
 
 /* Same with an explicit schedule (NULL = defaults). */
