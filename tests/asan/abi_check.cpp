@@ -48,6 +48,138 @@ void write_file(const std::string& path, const void* p, size_t n)
     std::fclose(f);
 }
 
+uint64_t mix(uint64_t x)
+{
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+// with a GPU (tests/test_asan_gpu.py): every host buffer path of the decode
+// entry points runs for real under ASan -- staging copies, the next-chunk
+// helper thread, packed hard bits unpacked into aligned and unaligned output,
+// posteriors, coded input from pageable and pinned memory, two shards, the
+// integer decoders, an irregular graph whose N is not a multiple of 8, the
+// engine, the DNA kernels.  Consistency: valid <=> zero syndrome, identical
+// results through the different entry points.
+void gpu_section(const std::string& pchk)
+{
+    int err = 0;
+    // irregular graph: N = 13, an empty column, degree-1 and empty rows
+    const int32_t rr[] = {0, 0, 0, 1, 1, 2, 3, 3, 3, 3, 4};
+    const int32_t cc[] = {0, 3, 7, 1, 12, 5, 2, 6, 8, 11, 9};
+    ldpc_graph* ig = ldpc_graph_from_edges(6, 13, rr, cc, 11, &err);
+    if (!ig) { expect("irregular graph", err, LDPC_OK); return; }
+    ldpc_graph* g = ldpc_graph_load(pchk.c_str(), &err);
+    if (!g) { expect("load", err, LDPC_OK); return; }
+    auto check_valid = [&](const char* what, const ldpc_graph* gg, int64_t B, int64_t N, const uint8_t* hard,
+                           const uint8_t* valid) {
+        for (int64_t b = 0; b < B; b++)
+            if ((ldpc_graph_syndrome(gg, hard + b * N, nullptr) == 0) != (valid[b] != 0)) {
+                expect(what, 0, 1);
+                return;
+            }
+        g_n++;
+    };
+    for (int algo : {LDPC_ALGO_BP, LDPC_ALGO_MSA, LDPC_ALGO_QMSA, LDPC_ALGO_GALLAGER_A, LDPC_ALGO_GALLAGER_B2}) {
+        const int64_t B = 5, N = 13;
+        std::vector<double> x((size_t)(B * N));
+        for (size_t i = 0; i < x.size(); i++) x[i] = ((mix(i + 99) >> 40) % 7 == 0 ? -2.0 : 2.5) + (double)(i % 3);
+        std::vector<uint8_t> h((size_t)(B * N + 1)), v((size_t)B);
+        std::vector<int32_t> it((size_t)B);
+        std::vector<double> post((size_t)(B * N));
+        expect("irregular decode", ldpc_decode(ig, x.data(), B, 7, algo, h.data() + 1,
+                                               algo <= LDPC_ALGO_MSA ? post.data() : nullptr, it.data(), v.data(),
+                                               nullptr), LDPC_OK);
+        check_valid("irregular valid", ig, B, N, h.data() + 1, v.data());
+    }
+    const int64_t N = 18432;
+    // two PCIe chunks (> 4096 codewords), coded input and fp64 input of the same values
+    const int64_t B = 4100;
+    const double unit = std::log(49.0);
+    std::vector<int8_t> codes((size_t)(B * N));
+    for (size_t i = 0; i < codes.size(); i++) codes[i] = (mix(i) >> 11) * 0x1p-53 < 0.01 ? -1 : 1;
+    std::vector<double> table(256), x((size_t)(B * N));
+    for (int k = 0; k < 256; k++) table[(size_t)k] = (k - 128) * unit;
+    for (size_t i = 0; i < x.size(); i++) x[i] = table[(size_t)(codes[i] + 128)];
+    std::vector<uint8_t> h1((size_t)(B * N)), h2((size_t)(B * N + 3)), v1((size_t)B), v2((size_t)B);
+    std::vector<int32_t> i1((size_t)B), i2((size_t)B);
+    expect("big decode", ldpc_decode(g, x.data(), B, 4, LDPC_ALGO_BP, h1.data(), nullptr, i1.data(), v1.data(),
+                                     nullptr), LDPC_OK);
+    expect("big decode_codes", ldpc_decode_codes(g, codes.data(), table.data(), LDPC_IN_LLR, B, 4, LDPC_ALGO_BP,
+                                                 h2.data() + 3, nullptr, i2.data(), v2.data(), nullptr), LDPC_OK);
+    expect("fp64 == codes", std::memcmp(h1.data(), h2.data() + 3, h1.size()) == 0 && i1 == i2 && v1 == v2, 1);
+    check_valid("big valid", g, B, N, h1.data(), v1.data());
+    // pinned codes, posteriors, two shards on device 0
+    const int64_t Bp = 300;
+    int8_t* pc = (int8_t*)ldpc_host_alloc((size_t)(Bp * N));
+    if (!pc) { expect("host alloc", 0, 1); return; }
+    std::memcpy(pc, codes.data(), (size_t)(Bp * N));
+    std::vector<double> post((size_t)(Bp * N));
+    ldpc_opts o{};
+    o.exp_on_host = 1;
+    o.n_devices = 2;
+    const int32_t devs[2] = {0, 0};
+    o.devices = devs;
+    std::vector<uint8_t> h3((size_t)(Bp * N)), v3((size_t)Bp);
+    std::vector<int32_t> i3((size_t)Bp);
+    expect("pinned two-shard decode", ldpc_decode_codes(g, pc, table.data(), LDPC_IN_LLR, Bp, 4, LDPC_ALGO_MSA,
+                                                        h3.data(), post.data(), i3.data(), v3.data(), &o), LDPC_OK);
+    check_valid("pinned valid", g, Bp, N, h3.data(), v3.data());
+    ldpc_host_free(pc);
+    // the engine: device BSC codes, coded decode, stats
+    ldpc_engine* e = ldpc_engine_create(g, 0, LDPC_ALGO_BP, 0, &err);
+    expect("engine", e ? 0 : err, 0);
+    if (e) {
+        const int64_t Be = 200;
+        std::vector<uint8_t> cw((size_t)N, 0);
+        void* d_cw = ldpc_dev_malloc(0, (size_t)N);
+        void* d_c = ldpc_dev_malloc(0, (size_t)(Be * N));
+        void* d_h = ldpc_dev_malloc(0, (size_t)(Be * N));
+        void* d_i = ldpc_dev_malloc(0, (size_t)Be * 4);
+        void* d_v = ldpc_dev_malloc(0, (size_t)Be);
+        ldpc_kernel_stats st{};
+        expect("engine run", ldpc_dev_memcpy(0, d_cw, cw.data(), (size_t)N, LDPC_H2D) ||
+                                  ldpc_engine_profile(e, 1) ||
+                                  ldpc_engine_gen_bsc_codes(e, (int8_t*)d_c, 0, Be, (const uint8_t*)d_cw, 1, 5, 0.004) ||
+                                  ldpc_engine_decode_codes(e, (const int8_t*)d_c, table.data(), LDPC_IN_LLR, Be, 10,
+                                                           (uint8_t*)d_h, nullptr, LDPC_POST_LLR, (int32_t*)d_i,
+                                                           (uint8_t*)d_v) ||
+                                  ldpc_engine_sync(e) || ldpc_engine_stats(e, &st),
+               LDPC_OK);
+        std::vector<uint8_t> he((size_t)(Be * N)), ve((size_t)Be);
+        ldpc_dev_memcpy(0, he.data(), d_h, he.size(), LDPC_D2H);
+        ldpc_dev_memcpy(0, ve.data(), d_v, ve.size(), LDPC_D2H);
+        check_valid("engine valid", g, Be, N, he.data(), ve.data());
+        for (void* p : {d_cw, d_c, d_h, d_i, d_v}) ldpc_dev_free(0, p);
+        ldpc_engine_free(e);
+    }
+    // the DNA kernels: one strand read twice, one read once (short), codes
+    const int32_t kind[3] = {1, 2, 0};
+    const int64_t rptr[4] = {0, 2, 3, 3};
+    std::vector<uint8_t> rows(3 * 136, 'A');
+    rows[136 + 5] = 'T';
+    const int32_t q[3] = {70, 40, 80};
+    std::vector<double> dl(2 * 136 * 3);
+    std::vector<uint8_t> dm(dl.size());
+    std::vector<int8_t> dc(dl.size());
+    int32_t exact = -1;
+    expect("dna llr codes", ldpc_dna_llr_codes(3, kind, rptr, rows.data(), q, 136, unit, dl.data(), dm.data(),
+                                               dc.data(), &exact, 0), LDPC_OK);
+    bool same = exact == 1;
+    for (size_t i = 0; i < dl.size(); i++) same = same && dl[i] == dc[i] * unit;
+    expect("dna codes == llr / unit", same ? 1 : 0, 1);
+    const char* sq = "ACGTACGTTTACGAACGT";
+    const int64_t off[3] = {0, 4, 9};
+    const int32_t len[3] = {4, 5, 9}, pa[2] = {0, 1}, pb[2] = {1, 2};
+    int32_t dist[2] = {-1, -1};
+    expect("edit distance", ldpc_dna_edit_distance((const uint8_t*)sq, off, len, 3, pa, pb, 2, dist, 0), LDPC_OK);
+    expect("edit distance values", dist[0] == 1 && dist[1] == 5, 1);  // Levenshtein, def_func.edit_dist
+    ldpc_graph_free(g);
+    ldpc_graph_free(ig);
+}
+
 }  // namespace
 
 int main(int argc, char** argv)
@@ -276,6 +408,7 @@ int main(int argc, char** argv)
     ldpc_graph_free(g);
     ldpc_graph_free(small);
     ldpc_graph_free(rs);
+    if (ndev > 0) gpu_section(pchk);
     std::printf("ok abi %d checks, %d device(s)\n", g_n, ndev);
     return g_bad ? 3 : 0;
 }

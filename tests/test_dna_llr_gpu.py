@@ -103,3 +103,22 @@ def test_full_scale_reads_decode(gpu, codewords):
     assert built.codes is not None and built.codes.dtype == np.int8
     assert np.array_equal(built.code_table()[built.codes.astype(np.int64) + 128], built.llr)
     assert 0 < res["n_erased_strands"] < 18432 * 0.05
+
+
+def test_build_llr_codes_beyond_int8(gpu, codewords):
+    """A strand read more than 127 times has count differences that no int8
+    code holds: ldpc_dna_llr_codes reports exact = 0, LlrResult.codes is
+    None, and the pipeline's first decode takes the fp64 entry instead."""
+    import dna_pipeline
+    idx, seqs, quals = synth.dna_reads(codewords, seed=31, n_reads=4000)
+    pay = synth.strand_payloads(codewords)
+    s0 = int(dna_llr.strand_indices()[0])
+    idx += [s0] * 140
+    seqs += [pay[0].tobytes().decode()] * 140
+    quals += [70] * 140
+    res = dna_llr.build_llr(idx, seqs, quals, eps=0.02, align_fn=dna_llr.pad_align)
+    assert res.codes is None
+    k = res.llr / math.log(49.0)
+    assert np.abs(k).max() > 127 and np.array_equal(k, np.rint(k))
+    t = dna_pipeline.trial_from_reads((idx, seqs, quals), codewords, eps=0.02, align_fn=dna_llr.pad_align)
+    assert t["first_success"] + len(t["fail_first"]) == 272
