@@ -73,13 +73,17 @@ void gpu_section(const std::string& pchk)
     if (!ig) { expect("irregular graph", err, LDPC_OK); return; }
     ldpc_graph* g = ldpc_graph_load(pchk.c_str(), &err);
     if (!g) { expect("load", err, LDPC_OK); return; }
-    auto check_valid = [&](const char* what, const ldpc_graph* gg, int64_t B, int64_t N, const uint8_t* hard,
+    auto check_valid = [&](const std::string& what, const ldpc_graph* gg, int64_t B, int64_t N, const uint8_t* hard,
                            const uint8_t* valid) {
-        for (int64_t b = 0; b < B; b++)
-            if ((ldpc_graph_syndrome(gg, hard + b * N, nullptr) == 0) != (valid[b] != 0)) {
-                expect(what, 0, 1);
+        for (int64_t b = 0; b < B; b++) {
+            const int syn = ldpc_graph_syndrome(gg, hard + b * N, nullptr);
+            if ((syn == 0) != (valid[b] != 0)) {
+                std::printf("MISMATCH %s: codeword %lld syndrome %d valid %d\n", what.c_str(), (long long)b, syn,
+                            (int)valid[b]);
+                g_bad = 1;
                 return;
             }
+        }
         g_n++;
     };
     for (int algo : {LDPC_ALGO_BP, LDPC_ALGO_MSA, LDPC_ALGO_QMSA, LDPC_ALGO_GALLAGER_A, LDPC_ALGO_GALLAGER_B2}) {
@@ -89,10 +93,10 @@ void gpu_section(const std::string& pchk)
         std::vector<uint8_t> h((size_t)(B * N + 1)), v((size_t)B);
         std::vector<int32_t> it((size_t)B);
         std::vector<double> post((size_t)(B * N));
-        expect("irregular decode", ldpc_decode(ig, x.data(), B, 7, algo, h.data() + 1,
+        expect(("irregular decode, algo " + std::to_string(algo)).c_str(), ldpc_decode(ig, x.data(), B, 7, algo, h.data() + 1,
                                                algo <= LDPC_ALGO_MSA ? post.data() : nullptr, it.data(), v.data(),
                                                nullptr), LDPC_OK);
-        check_valid("irregular valid", ig, B, N, h.data() + 1, v.data());
+        check_valid("irregular valid, algo " + std::to_string(algo), ig, B, N, h.data() + 1, v.data());
     }
     const int64_t N = 18432;
     // two PCIe chunks (> 4096 codewords), coded input and fp64 input of the same values
