@@ -39,6 +39,10 @@
 #include "../../include/ldpc_amd.h"
 #include "cli_io.hpp"
 
+// the loaded graph, freed at exit on every path (die() exits directly)
+static ldpc_graph* g_graph = nullptr;
+static void free_graph() { if (g_graph) ldpc_graph_free(g_graph); g_graph = nullptr; }
+
 static void die(const char* msg)
 {
     std::fprintf(stderr, "%s\n", msg);
@@ -123,6 +127,8 @@ int main(int argc, char** argv)
     // ---- Set_Code (DNA_main.cpp:544-609) ----
     int err = 0;
     ldpc_graph* g = ldpc_graph_load(file_pchk.c_str(), &err);
+    g_graph = g;
+    std::atexit(free_graph);
     if (!g) { std::fprintf(stderr, "%s\n", ldpc_last_error()); return 1; }
     int32_t M, N, dv, rdv, dc, rdc;
     int64_t E;
@@ -315,7 +321,7 @@ int main(int argc, char** argv)
     for (int i = 0; i < 2; i++) std::fprintf(fr, "BER[%2d]                 : %.5e\n", i, BER[i]);
     std::fprintf(fr, "\n");
     std::fclose(fr);
-    ldpc_graph_free(g);
+    free_graph();
     (void)iters; (void)valid;
     return 0;
 }

@@ -33,3 +33,42 @@ def test_c_abi_sanitized_on_gpu(gpu, tmp_path):
     assert r.returncode == 0, (r.returncode, r.stdout[-3000:], r.stderr[-3000:])
     out = r.stdout.strip()
     assert out.startswith("ok abi ") and "device(s)" in out and not out.endswith(" 0 device(s)"), out
+
+
+@pytest.mark.timeout(300)
+def test_cli_sanitized_on_gpu(gpu, tmp_path, codewords):
+    """bin/ldpc's code over the sanitized library (tests/asan/build/ldpc_asan),
+    end to end on the MI355X: for BP, min-sum, puncturing and shortening
+    argv forms it writes the same dec_ file and result file (bar the clock
+    lines) as the product's bin/ldpc, with no sanitizer report."""
+    import shutil
+    import synth
+    exe_san = os.path.join(ASAN, "build", "ldpc_asan")
+    exe = os.path.join(ROOT, "dna-ldpc-codes_amd", "bin", "ldpc")
+    assert os.access(exe_san, os.X_OK) and os.access(exe, os.X_OK)
+    llr = synth.bsc_llrs(codewords, 0, 1, seed=21, p=0.01)[0]
+    env = dict(os.environ,
+               ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:abort_on_error=0:exitcode=97",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1:exitcode=98",
+               LSAN_OPTIONS="suppressions=" + os.path.join(ASAN, "lsan.supp"))
+    forms = [["0", "0", "0", "7", "30", "1", "C", "S", "P", "0", "0", "0", "0"],
+             ["0", "20", "0", "7", "30", "1", "C", "S", "P", "0", "0", "0", "0"],
+             ["0", "0", "0", "7", "30", "2", "C", "S", "P", "0", "1", "0", "1", "100", "400", "1", "9000"],
+             ["0", "0", "0", "7", "30", "1", "C", "S", "P", "1.0", "0", "1", "0", "5000", "5100"]]
+    for i, argv in enumerate(forms):
+        outs = []
+        for tag, binary in (("san", exe_san), ("ref", exe)):
+            d = tmp_path / f"{i}_{tag}"
+            d.mkdir()
+            shutil.copyfile(PCHK, d / "P.pchk")
+            (d / "C.txt").write_text("".join(f"{int(b)} " for b in codewords[0]))
+            (d / "S.txt").write_text("".join(str(float(v)) + " " for v in llr))
+            r = subprocess.run([binary, *argv], cwd=d, capture_output=True, text=True, env=env, timeout=120)
+            assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr \
+                and "ERROR: LeakSanitizer" not in r.stderr, (argv, r.stderr[-4000:])
+            assert r.returncode == 0, (tag, argv, r.stderr[-2000:])
+            res = [p for p in os.listdir(d) if p.startswith("result_")]
+            assert len(res) == 1
+            txt = [l for l in open(d / res[0]).read().splitlines() if "time" not in l]
+            outs.append(((d / "dec_C.txt").read_bytes(), txt, res[0]))
+        assert outs[0] == outs[1], argv

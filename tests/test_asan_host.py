@@ -313,3 +313,44 @@ def test_cli_refuses_bad_inputs(tmp_path):
     for argv, msg in cases:
         r = subprocess.run(argv, cwd=d, capture_output=True, text=True, timeout=120)
         assert r.returncode == 1 and msg in r.stderr, (argv, r.returncode, r.stderr)
+
+
+CLI_ARGV = [  # (argv after the program name, with C = codeword base, S = soft base, P = pchk base)
+    ["0", "0", "0", "7", "5", "1", "C", "S", "P", "0", "0", "0", "0"],
+    ["0", "20", "1", "7", "5", "3", "C", "S", "P", "0.02", "1", "0", "0", "100", "400"],      # BSC, puncturing 1
+    ["1", "0", "0", "7", "5", "0", "4", "C", "S", "P", "1.5", "0", "1", "1", "5000", "5100", "1", "18432"],
+    ["0", "0", "0", "7", "5", "1", "C", "S", "P", "0", "2", "0", "0", "10", "20", "2", "3"],  # SC puncturing 2
+    ["0", "0", "0", "7", "5", "1", "C", "S", "P", "0", "4", "0", "0", "1", "2", "3", "4", "2", "3", "5", "6"],
+    ["0", "0", "2", "7", "5", "1", "C", "S", "P", "0.1", "0", "2", "0", "3", "2"],           # BEC, shortening 2
+    ["0", "1", "0", "7", "5", "1", "C", "S", "P", "0", "0", "0", "1", "1", "18432"],         # Gallager A, targeting
+    ["0", "99", "0", "7", "5", "1", "C", "S", "P", "0", "0", "0", "0"],                      # unknown decoder
+    ["0", "0", "0", "7", "5", "1", "C", "S", "P", "0", "0", "0", "1", "0", "5"],             # target_VN outside
+    ["0", "0", "0", "7", "5", "1", "C", "S", "P", "0", "2", "0", "0", "10", "20", "2", "-5"], # SC L < 0
+    ["0", "0", "0", "7", "5", "1", "C", "S", "P", "0", "1", "0", "0", "1", "99999"],         # punctured bit outside
+    ["0", "0", "0", "7", "5", "1", "C", "S", "P", "0"],                                      # too few arguments
+]
+
+
+@pytest.mark.timeout(600)
+def test_cli_sanitized_argv_paths(tmp_path):
+    """bin/ldpc's own code (argv parsing, SC side files, code-rate and
+    puncturing / shortening bookkeeping, the input readers) under ASan +
+    UBSan, linked against the sanitized library: every argv form either
+    refuses its arguments (exit 1 with a message) or reaches the decode,
+    which has no GPU here (exit 1, "decode failed"); no sanitizer report.
+    tests/test_asan_gpu.py runs the same binary end to end on the MI355X."""
+    if not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("no hipcc")
+    subprocess.run(["make", "-s", "-j", "8", "-C", ASAN_DIR, "abi"], check=True, capture_output=True, timeout=900)
+    exe = os.path.join(ASAN_DIR, "build", "ldpc_asan")
+    d = tmp_path
+    shutil.copyfile(PCHK, d / "P.pchk")
+    (d / "C.txt").write_text("0 " * 18432)
+    (d / "S.txt").write_text("3.8918202981106265 " * 18432)
+    (d / "P.txt").write_text("256 512 1024 7 7 9 9\n")  # SC multiplicities for the type 2-4 forms
+    env = dict(os.environ, **SAN_ENV)
+    for argv in CLI_ARGV:
+        r = subprocess.run([exe, *argv], cwd=d, capture_output=True, text=True, env=env, timeout=120)
+        assert "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, (argv, r.stderr[-3000:])
+        assert r.returncode == 1, (argv, r.returncode, r.stderr[-1000:])
+        assert r.stderr.strip(), argv  # a message, never a silent exit
