@@ -33,11 +33,11 @@ using ldpc::Engine;
 using ldpc::HostGraph;
 using ldpc::set_error;
 
+constexpr int kMaxDevices = 64;       // opts.n_devices bound (one host thread per device)
+constexpr int kMaxHostThreads = 256;  // opts.host_threads clamp
 // shards up to this many codewords get a lane pool holding all of them
 // (the 272-codeword DNA batch: 248k cw/s grouped vs 194k through the
 // resident pool); larger ones use the engine's own pool
-constexpr int kMaxDevices = 64;       // opts.n_devices bound (one host thread per device)
-constexpr int kMaxHostThreads = 256;  // opts.host_threads clamp
 constexpr int64_t kExplicitPoolMax = 1024;
 constexpr int64_t kXferChunk = 4096;  // codewords per PCIe chunk (at least); shards of <= kExplicitPoolMax
                                       // cross in one chunk (A/B on the DNA batch: chunks of 128 or 192
