@@ -54,16 +54,28 @@ struct IntParams {
     int32_t b_dec;      // Gallager: decision threshold
 };
 
+// int32 arithmetic with the reference's wrap-around.  The reference is an
+// x86 build: (int) of a double outside the int32 range -- an infinite or NaN
+// LLR, or |LLR| / step >= 2^31 -- converts (cvttsd2si) to INT32_MIN, the
+// "integer indefinite" value, which its sign step, abs() and sums then carry
+// with two's-complement wrap.  In C++ all of these are undefined and the
+// device's own conversion saturates, so the cases are spelled out here (and
+// identically in oracle/ldpc_oracle.c).
+__device__ __forceinline__ int32_t wrap_neg(int32_t v) { return (int32_t)(0u - (uint32_t)v); }
+__device__ __forceinline__ int32_t wrap_add(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+__device__ __forceinline__ int32_t wrap_sub(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+
 // Cal_MSA_Q(x, 0): uniform quantizer with clipping (dec.cpp:1708-1746)
 __device__ __forceinline__ int32_t quantize(double x, const IntParams& p)
 {
     const double mag = __builtin_fabs(x);
-    int32_t k = (int32_t)(mag / p.step + 0.5);
+    const double q = mag / p.step + 0.5;
+    int32_t k = q < 2147483648.0 ? (int32_t)q : INT32_MIN;  // (NaN fails the compare)
     if (x >= 0) {
         if (k > p.max_value) k = p.max_value;
     } else {
         if (k > -p.min_value) k = -p.min_value;
-        k = -k;
+        k = wrap_neg(k);  // k *= sign
     }
     return k;
 }
@@ -142,7 +154,7 @@ __global__ __launch_bounds__(256) void k_check_int(const int32_t* __restrict__ v
     uint32_t neg = 0;
     for (int32_t e = a; e < b; ++e) {
         const int32_t x = v2c[(tb + e) * TILE + lane];
-        const int32_t ax = x < 0 ? -x : x;
+        const int32_t ax = x < 0 ? wrap_neg(x) : x;  // abs(), INT32_MIN stays INT32_MIN
         neg ^= x >= 0 ? 0u : 1u;
         if (ax < m1) { m2 = m1; m1 = ax; i1 = e; }
         else if (ax < m2) m2 = ax;
@@ -151,7 +163,7 @@ __global__ __launch_bounds__(256) void k_check_int(const int32_t* __restrict__ v
         const int32_t x = v2c[(tb + e) * TILE + lane];
         // mag_min over the other edges; -1 sentinel when there are none
         int32_t mag = (b - a == 1) ? -1 : (e == i1 ? m2 : m1);
-        mag -= p.beta;
+        mag = wrap_sub(mag, p.beta);
         if (mag < 0) mag = 0;
         const int32_t sign = ((neg ^ (x >= 0 ? 0u : 1u)) & 1u) ? -1 : 1;
         c2v[(tl + e) * TILE + lane] = sign * mag;
@@ -182,15 +194,17 @@ __global__ __launch_bounds__(256) void k_var_int(const int32_t* __restrict__ c2v
         const size_t pj = ((size_t)t * N + j) * TILE + lane;
         const int32_t pr = prior[pj];
         if (p.algo == LDPC_ALGO_QMSA) {
+            // the reference's sequential sum prior + the other edges, in wrapping
+            // int32 (associative, so prior + all - own is the same value)
             int32_t tot = 0;
-            for (int32_t s = a; s < b; ++s) tot += c2v[(tl + col_edge[s]) * TILE + lane];
+            for (int32_t s = a; s < b; ++s) tot = wrap_add(tot, c2v[(tl + col_edge[s]) * TILE + lane]);
             for (int32_t s = a; s < b; ++s) {
-                int32_t sum = pr + tot - c2v[(tl + col_edge[s]) * TILE + lane];
+                int32_t sum = wrap_sub(wrap_add(pr, tot), c2v[(tl + col_edge[s]) * TILE + lane]);
                 if (sum > p.max_value) sum = p.max_value;
                 else if (sum < p.min_value) sum = p.min_value;
                 v2c[(tb + col_edge[s]) * TILE + lane] = sum;
             }
-            const int32_t L = pr + tot;
+            const int32_t L = wrap_add(pr, tot);
             h = L > 0 ? false : (L < 0 ? true : tie_bit(p.seed, b_base + t * TILE + lane, iter + 1, j));
             if (post) post[pj] = (double)L;
         } else {

@@ -27,6 +27,7 @@
  *
  * Build: oracle/Makefile  (gcc -O2 -ffp-contract=off, no fast-math).
  */
+#include <limits.h>
 #include <math.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -445,16 +446,25 @@ typedef struct {
 } int_params;
 
 /* Cal_MSA_Q(x, 0), dec.cpp:1708-1746 */
+/* int arithmetic with the reference's wrap-around: it is an x86 build, where
+ * (int) of a double outside the int range (an infinite or NaN LLR, or
+ * |LLR| / step >= 2^31) converts to INT_MIN ("integer indefinite", cvttsd2si)
+ * and abs() / sign products / sums of INT_MIN wrap.  All undefined in C, so
+ * spelled out (and identically in the product, kernels_int.hpp). */
+static int wrap_neg(int v) { return (int)(0u - (unsigned)v); }
+static int wrap_add(int a, int b) { return (int)((unsigned)a + (unsigned)b); }
+
 static int cal_msa_q(double x, const int_params *p)
 {
     int k, sign = x >= 0 ? 1 : -1;
     double mag = fabs(x);
-    k = (int)(mag / p->step + 0.5);
+    double q = mag / p->step + 0.5;
+    k = q < 2147483648.0 ? (int)q : INT_MIN; /* (NaN fails the compare) */
     if (sign == 1) {
         if (k > p->max_value) k = p->max_value;
     } else {
         if (k > -p->min_value) k = -p->min_value;
-        k *= sign;
+        k = wrap_neg(k); /* k *= sign */
     }
     return k;
 }
@@ -496,11 +506,11 @@ static int int_decode_one(const oracle_graph *g, const double *llr, int max_iter
                     int mag_min = -1, sign = 1;
                     for (int f = g->row_ptr[i]; f < g->row_ptr[i + 1]; f++) {
                         if (g->col_idx[e] == g->col_idx[f]) continue;
-                        int a = abs(v2c[f]);
+                        int a = v2c[f] < 0 ? wrap_neg(v2c[f]) : v2c[f]; /* abs(INT_MIN) = INT_MIN */
                         if (mag_min == -1 || mag_min > a) mag_min = a;
                         sign *= v2c[f] >= 0 ? 1 : -1;
                     }
-                    mag_min = mag_min - p->beta;
+                    mag_min = wrap_add(mag_min, wrap_neg(p->beta));
                     if (mag_min < 0) mag_min = 0;
                     c2v[e] = sign * mag_min;
                 } else {
@@ -519,7 +529,7 @@ static int int_decode_one(const oracle_graph *g, const double *llr, int max_iter
                 for (int s = a0; s < a1; s++) {
                     int e = g->col_edge[s], sum = prior[j];
                     for (int r = a0; r < a1; r++)
-                        if (g->col_edge[r] != e) sum += c2v[g->col_edge[r]];
+                        if (g->col_edge[r] != e) sum = wrap_add(sum, c2v[g->col_edge[r]]);
                     v2c[e] = cal_msa_clip(sum, p);
                 }
             } else {
@@ -538,7 +548,7 @@ static int int_decode_one(const oracle_graph *g, const double *llr, int max_iter
             if (p->algo == 2) {
                 /* Decision_MSA dec.cpp:1624-1656 */
                 int sum = prior[j];
-                for (int s = a0; s < a1; s++) sum += c2v[g->col_edge[s]];
+                for (int s = a0; s < a1; s++) sum = wrap_add(sum, c2v[g->col_edge[s]]);
                 post[j] = (double)sum;
                 dblk[j] = sum > 0 ? 0 : (sum < 0 ? 1 : (uint8_t)tie_bit(p->seed, b, n + 1, j));
             } else {

@@ -579,8 +579,15 @@ int do_decode(const std::string& path, int algo, int iters, uint64_t seed, doubl
     std::printf("ok decode algo=%d iters=%d valid=%d ones=%d syndrome=%d\n", algo, it, valid, flips, sa);
     // the integer-message decoders of the oracle (quantized / offset min-sum,
     // Gallager A / B1 / B2): valid flags must agree with the host syndrome
+    // (with infinite, NaN and huge inputs: the quantizer's out-of-range
+    // conversion and the wrapping int sums, defined in the oracle)
+    std::vector<double> xl(llr);
+    xl[5] = INFINITY;
+    xl[6] = -INFINITY;
+    xl[(size_t)N + 7] = NAN;
+    xl[(size_t)N + 8] = 1e300;
     for (int ialgo = 2; ialgo <= 5; ialgo++) {
-        oracle_decode_int_batch(&o, llr.data(), B, iters, ialgo, 6, 0.5, 1, seed, 2, hard.data(), nullptr, ib.data(),
+        oracle_decode_int_batch(&o, xl.data(), B, iters, ialgo, 6, 0.5, 1, seed, 2, hard.data(), nullptr, ib.data(),
                                 vb.data());
         for (int b = 0; b < B; b++)
             if ((ldpc::syndrome_host(g, hard.data() + (size_t)b * N, nullptr) == 0) != (vb[(size_t)b] != 0))

@@ -107,3 +107,40 @@ def test_reference_decoder_type_ints(gpu, G, codewords):
         for x, y in zip(a, b):
             if x is not None:
                 assert np.array_equal(np.asarray(x), np.asarray(y)), (t, name)
+
+
+def test_oracle_quantizer_out_of_range(og_int, codewords):
+    """Cal_MSA_Q (dec.cpp:1708-1746) on values outside the int range: the
+    reference's x86 build converts them to INT_MIN (cvttsd2si's "integer
+    indefinite"), whatever their sign, and its sign step keeps INT_MIN -- so
+    an infinite, NaN or huge LLR enters quantized min-sum as a strongly
+    negative prior (bit decided 1), never as +max_value.  The oracle spells
+    this out (no C undefined behaviour); a 0-iteration decode shows the
+    quantized priors directly."""
+    llr = np.where(codewords[:1] == 1, -L49, L49)
+    bad = {3: np.inf, 4: -np.inf, 5: np.nan, 6: 1e300, 7: -1e300, 8: 2.0 ** 31 * 0.5, 9: 2.0 ** 30 - 0.5}
+    for j, x in bad.items():
+        llr[0, j] = x
+    _, post, _, _ = og_int.decode_int_batch(llr, 0, 2, precision=6, step=0.5)
+    int_min = float(-2 ** 31)
+    for j in (3, 4, 5, 6, 7, 8):
+        assert post[0, j] == int_min, (j, post[0, j])
+    assert post[0, 9] == 31.0  # in range: clipped to max_value = 2^(6-1) - 1
+
+
+@pytest.mark.gpu
+def test_int_decoders_out_of_range_inputs(gpu, G, og_int, codewords):
+    """The same out-of-range LLRs through every integer decoder on the GPU,
+    bit-exact against the oracle (quantizer + wrapping int sums,
+    kernels_int.hpp)."""
+    llr = synth.bsc_llrs(codewords, 0, 70, seed=33, p=0.004)
+    rng = np.random.default_rng(4)
+    for x in (np.inf, -np.inf, np.nan, 1e300, -1e300, 2.0 ** 31 * 0.5):
+        idx = rng.integers(0, llr.size, 40)
+        llr.flat[idx] = x
+    for algo, name in ((2, "qmsa"), (3, "gallager_a"), (4, "gallager_b1"), (5, "gallager_b2")):
+        for beta in ((0, 1) if algo == 2 else (0,)):
+            rh, rpost, rit, rv = og_int.decode_int_batch(llr, 15, algo, precision=6, step=0.5, beta=beta)
+            h, post, it, v = G.decode(llr, max_iter=15, algo=name, post="llr", msa_offset=beta)
+            assert np.array_equal(h, rh) and np.array_equal(it, rit) and np.array_equal(v, rv.astype(bool)), name
+            assert np.array_equal(post, rpost), name

@@ -1,0 +1,112 @@
+"""GPU parity on random codes: a seeded sweep of parity-check matrices the
+DNA code never exercises -- single rows, N not a multiple of 8 or 64, rows
+heavier than 72, empty rows and columns, duplicate entries -- and random
+(dv, dc) = (8, 72)-regular codes that are not array codes (the specialised
+degree-72 kernels on an unstructured graph).  Each graph is written as a
+.pchk and loaded on both sides (mod2sparse_read, mod2sparse.cpp:381-427);
+BP (dec.cpp:583-694) and min-sum (dec.cpp:1216-1678) decodes must equal the
+oracle bit for bit: hard decisions, iteration counts, valid flags and the
+posterior (BP likelihood ratio, min-sum L), over ragged batches, max_iter 0
+and erasures / infinities in the channel input; the integer decoders
+(dec.cpp:699-832, 1174-1764) on a subset."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import _cmp, _write_pchk
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_graph(rng, M, N, deg_lo, deg_hi, dup=True):
+    rows, cols = [], []
+    for i in range(M):
+        d = int(rng.integers(deg_lo, deg_hi + 1))
+        for j in rng.choice(N, size=min(d, N), replace=False):
+            rows.append(i)
+            cols.append(int(j))
+    if dup and rows:
+        k = int(rng.integers(0, len(rows)))
+        rows.append(rows[k])
+        cols.append(cols[k])  # a duplicate entry: ignored (mod2sparse.cpp:521-524)
+    return rows, cols
+
+
+def _regular_graph(rng, Q, dv=8, dc=72):
+    """A random (dv, dc)-regular code with M = dv * Q rows and N = dc * Q
+    columns: row block b holds each column once (a random permutation per
+    block), so no column repeats in a row and every degree is exact."""
+    M, N = dv * Q, dc * Q
+    rows, cols = [], []
+    for b in range(dv):
+        perm = rng.permutation(N)
+        for i in range(Q):
+            for j in perm[i * dc:(i + 1) * dc]:
+                rows.append(b * Q + i)
+                cols.append(int(j))
+    return M, N, rows, cols
+
+
+def _llr(rng, B, N, kind):
+    if kind == "normal":
+        x = rng.normal(1.5, 2.5, size=(B, N))
+    else:  # lattice +-ln49 from a BSC, with erasures and infinities
+        x = np.where(rng.random((B, N)) < 0.03, -3.8918202981106265, 3.8918202981106265)
+        x[rng.random((B, N)) < 0.02] = 0.0
+        if B > 2:
+            x[1, 0] = np.inf
+            x[2, N - 1] = -np.inf
+    return np.ascontiguousarray(x)
+
+
+CASES = [  # (M, N, row degree range, B, max_iter, llr kind)
+    (1, 2, (2, 2), 1, 5, "normal"),
+    (1, 9, (9, 9), 3, 3, "lattice"),
+    (3, 17, (1, 6), 65, 0, "normal"),
+    (17, 63, (2, 9), 64, 12, "lattice"),
+    (24, 64, (3, 12), 63, 20, "normal"),
+    (30, 65, (1, 20), 130, 25, "lattice"),
+    (40, 130, (0, 7), 7, 30, "normal"),
+    (12, 500, (60, 110), 70, 15, "lattice"),   # rows heavier than 72
+    (200, 500, (2, 6), 129, 40, "normal"),
+    (64, 1001, (5, 30), 66, 25, "lattice"),
+]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_random_graph_bitexact(gpu, oracle_mod, tmp_path, case):
+    M, N, (lo, hi), B, max_iter, kind = CASES[case]
+    rng = np.random.default_rng(1000 + case)
+    rows, cols = _random_graph(rng, M, N, lo, hi)
+    path = tmp_path / f"rand{case}.pchk"
+    _write_pchk(path, M, N, rows, cols)
+    og = oracle_mod.OracleGraph(str(path))
+    G = gpu.Graph(str(path))
+    assert (G.M, G.N, G.E) == (og.M, og.N, og.E)
+    llr = _llr(rng, B, N, kind)
+    _cmp(G, og, llr, max_iter)
+    _cmp(G, og, llr, max_iter, algo="msa")
+    if case % 3 == 0:  # the integer decoders: Gallager A / B1 / B2 and quantized min-sum
+        for algo, name in ((3, "gallager_a"), (4, "gallager_b1"), (5, "gallager_b2"), (2, "qmsa")):
+            rh, _, rit, rv = og.decode_int_batch(llr, max_iter, algo)
+            h, _, it, v = G.decode(llr, max_iter=max_iter, algo=name, post=None)
+            assert np.array_equal(h, rh) and np.array_equal(it, rit) and np.array_equal(v, rv.astype(bool)), name
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("Q", [2, 5, 16])
+def test_random_regular_8_72_bitexact(gpu, oracle_mod, tmp_path, Q):
+    """(8, 72)-regular codes that are not array codes: the specialised
+    degree-72 check kernels and the default schedules on an unstructured
+    graph (ldpc_graph_blocks finds no block layout)."""
+    rng = np.random.default_rng(Q)
+    M, N, rows, cols = _regular_graph(rng, Q)
+    path = tmp_path / f"reg{Q}.pchk"
+    _write_pchk(path, M, N, rows, cols)
+    og = oracle_mod.OracleGraph(str(path))
+    G = gpu.Graph(str(path))
+    assert (G.dc, G.regular_dc, G.dv, G.regular_dv) == (72, True, 8, True)
+    for B, p, it in ((1, 0.01, 20), (64, 0.02, 30), (200, 0.005, 25)):
+        llr = np.where(rng.random((B, N)) < p, -3.8918202981106265, 3.8918202981106265)
+        _cmp(G, og, np.ascontiguousarray(llr), it)
+        _cmp(G, og, np.ascontiguousarray(llr), it, algo="msa")
