@@ -110,3 +110,40 @@ def test_random_regular_8_72_bitexact(gpu, oracle_mod, tmp_path, Q):
         llr = np.where(rng.random((B, N)) < p, -3.8918202981106265, 3.8918202981106265)
         _cmp(G, og, np.ascontiguousarray(llr), it)
         _cmp(G, og, np.ascontiguousarray(llr), it, algo="msa")
+
+
+SCHEDULES = [
+    {},                                            # defaults: resident pool (BP), compressed continuous (min-sum)
+    {"resident": False},                           # grouped continuous
+    {"resident": False, "nontemporal": True, "var_cpw": 8},
+    {"resident": False, "group_tiles": 1, "var_cpw": 1},
+    {"continuous": False},                         # fixed passes
+    {"msa_compressed": False},                     # fp64 min-sum messages
+    {"first_from_prior": False, "split_syndrome": False},
+]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("sch", range(len(SCHEDULES)))
+def test_random_regular_schedules_bitexact(gpu, oracle_mod, tmp_path, sch):
+    """Every schedule family on a random (8, 72)-regular code with N % 64 == 0
+    (the specialised kernels' fast paths), fp64 and coded input: a schedule
+    decides how the batch is laid out over launches, never what it computes."""
+    rng = np.random.default_rng(77)
+    M, N, rows, cols = _regular_graph(rng, 16)
+    path = tmp_path / "reg16.pchk"
+    _write_pchk(path, M, N, rows, cols)
+    og = oracle_mod.OracleGraph(str(path))
+    G = gpu.Graph(str(path))
+    schedule = SCHEDULES[sch]
+    B = 300
+    llr = np.ascontiguousarray(np.where(rng.random((B, N)) < 0.012, -3.8918202981106265, 3.8918202981106265))
+    llr[rng.random((B, N)) < 0.01] = 0.0
+    for algo in ("bp", "msa"):
+        h, p, it, v = _cmp(G, og, llr, 30, algo=algo, schedule=schedule)
+        codes = np.rint(llr / 3.8918202981106265).astype(np.int8)
+        table = np.arange(-128, 128, dtype=np.float64) * 3.8918202981106265
+        h2, p2, it2, v2 = G.decode_codes(codes, table, max_iter=30, algo=algo,
+                                         post="ratio" if algo == "bp" else "llr", schedule=schedule)
+        assert np.array_equal(h2, h) and np.array_equal(it2, it) and np.array_equal(v2, v)
+        assert np.array_equal(p2.view(np.uint64), p.view(np.uint64))
