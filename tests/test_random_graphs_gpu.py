@@ -7,7 +7,7 @@ degree-72 kernels on an unstructured graph).  Each graph is written as a
 BP (dec.cpp:583-694) and min-sum (dec.cpp:1216-1678) decodes must equal the
 oracle bit for bit: hard decisions, iteration counts, valid flags and the
 posterior (BP likelihood ratio, min-sum L), over ragged batches, max_iter 0
-and erasures / infinities in the channel input; the integer decoders
+and erasures / -0.0 / infinities / NaN in the channel input; the integer decoders
 (dec.cpp:699-832, 1174-1764) on a subset."""
 import numpy as np
 import pytest
@@ -15,6 +15,19 @@ import pytest
 from test_gpu_parity import _cmp, _write_pchk
 
 pytestmark = pytest.mark.gpu
+
+
+def _cmp_nan(G, og, llr, max_iter, algo="bp"):
+    """test_gpu_parity._cmp, with the NaN rule of test_nan_and_infinite_llrs:
+    a NaN posterior only has to be matched by a NaN (payload and sign are not
+    part of the contract); everything else bit for bit."""
+    a = 0 if algo == "bp" else 1
+    ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, max_iter, algo=a, post_mode=1 if a == 0 else 0, threads=8)
+    h, p, it, v = G.decode(llr, max_iter=max_iter, algo=algo, post="ratio" if a == 0 else "llr")
+    assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h), algo
+    nan = np.isnan(ref_p)
+    assert np.array_equal(np.isnan(p), nan), algo
+    assert np.array_equal(p[~nan].view(np.uint64), ref_p[~nan].view(np.uint64)), algo
 
 
 def _random_graph(rng, M, N, deg_lo, deg_hi, dup=True):
@@ -49,12 +62,15 @@ def _regular_graph(rng, Q, dv=8, dc=72):
 def _llr(rng, B, N, kind):
     if kind == "normal":
         x = rng.normal(1.5, 2.5, size=(B, N))
-    else:  # lattice +-ln49 from a BSC, with erasures and infinities
+    else:  # lattice +-ln49 from a BSC, with erasures, -0.0, infinities and a NaN
         x = np.where(rng.random((B, N)) < 0.03, -3.8918202981106265, 3.8918202981106265)
         x[rng.random((B, N)) < 0.02] = 0.0
+        x[rng.random((B, N)) < 0.01] = -0.0
         if B > 2:
             x[1, 0] = np.inf
             x[2, N - 1] = -np.inf
+        if B > 4:
+            x[4, N // 2] = np.nan
     return np.ascontiguousarray(x)
 
 
@@ -84,8 +100,8 @@ def test_random_graph_bitexact(gpu, oracle_mod, tmp_path, case):
     G = gpu.Graph(str(path))
     assert (G.M, G.N, G.E) == (og.M, og.N, og.E)
     llr = _llr(rng, B, N, kind)
-    _cmp(G, og, llr, max_iter)
-    _cmp(G, og, llr, max_iter, algo="msa")
+    _cmp_nan(G, og, llr, max_iter)
+    _cmp_nan(G, og, llr, max_iter, algo="msa")
     if case % 3 == 0:  # the integer decoders: Gallager A / B1 / B2 and quantized min-sum
         for algo, name in ((3, "gallager_a"), (4, "gallager_b1"), (5, "gallager_b2"), (2, "qmsa")):
             rh, _, rit, rv = og.decode_int_batch(llr, max_iter, algo)
