@@ -67,12 +67,24 @@ def main():
                 for v in (np.inf, -np.inf, np.nan, -0.0):
                     x[rng.random((B, N)) < 0.003] = v
         x = np.ascontiguousarray(x)
-        algo = "bp" if rng.random() < 0.5 else "msa"
+        r = rng.random()
+        algo = "bp" if r < 0.4 else "msa" if r < 0.8 else str(rng.choice(["qmsa", "gallager_a", "gallager_b1",
+                                                                          "gallager_b2"]))
         sch = SCHEDULES[int(rng.integers(0, len(SCHEDULES)))]
-        ai = 0 if algo == "bp" else 1
+        ai = {"bp": 0, "msa": 1, "qmsa": 2, "gallager_a": 3, "gallager_b1": 4, "gallager_b2": 5}[algo]
         try:
-            rh, rp, rit, rv = og.decode_batch(x, max_iter, algo=ai, post_mode=1 if ai == 0 else 0, threads=8)
-            h, ph, it, v = G.decode(x, max_iter=max_iter, algo=algo, post="ratio" if ai == 0 else "llr", schedule=sch)
+            if ai >= 2:  # integer decoders: random quantizer / offset / tie seed (Set_MSA dec.cpp:1683)
+                prec, step = int(rng.integers(2, 17)), float(rng.choice([0.25, 0.5, 1.0, 1.7]))
+                beta, seed = int(rng.integers(0, 3)), int(rng.integers(0, 1 << 30))
+                sch = {"prec": prec, "step": step, "beta": beta}
+                rh, rp, rit, rv = og.decode_int_batch(x, max_iter, ai, precision=prec, step=step, beta=beta, seed=seed,
+                                                      threads=8)
+                h, ph, it, v = G.decode(x, max_iter=max_iter, algo=algo, post="llr", msa_precision=prec,
+                                        msa_step=step, msa_offset=beta, tie_seed=seed)
+            else:
+                rh, rp, rit, rv = og.decode_batch(x, max_iter, algo=ai, post_mode=1 if ai == 0 else 0, threads=8)
+                h, ph, it, v = G.decode(x, max_iter=max_iter, algo=algo, post="ratio" if ai == 0 else "llr",
+                                        schedule=sch)
             nan = np.isnan(rp)
             ok = (np.array_equal(h, rh) and np.array_equal(it, rit) and np.array_equal(v, rv.astype(bool))
                   and np.array_equal(np.isnan(ph), nan) and np.array_equal(ph[~nan].view(np.uint64),
@@ -83,7 +95,7 @@ def main():
         if not ok:
             bad += 1
         print(f"case {c:3d} {'ok ' if ok else 'BAD'} {shape:>12} M={M:4d} N={N:4d} E={G.E:6d} B={B:3d} "
-              f"it={max_iter:2d} in={kind} {algo:3s} {sch}", flush=True)
+              f"it={max_iter:2d} in={kind} {algo:11s} {sch}", flush=True)
     print(f"soak: {bad} mismatching case(s)", flush=True)
     sys.exit(1 if bad else 0)
 
