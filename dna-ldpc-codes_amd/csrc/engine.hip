@@ -452,6 +452,18 @@ int Engine::collect_stats()
 #define LAUNCH(cls, ...) LAUNCH_ON(stream, cls, __VA_ARGS__)
 
 // check phase of tiles t0 .. t0+gt-1 into `scratch` (that group's c2v); with
+// Degree buckets of the register-staged generic kernels (kernels.hpp *_gr):
+// the smallest bucket >= the graph's maximum degree, 0 when none holds it
+// (the memory-staged *_gen kernels then run).
+static constexpr int kGenCheckBuckets[] = {8, 16, 32, 48, 64, 96, 0};
+static constexpr int kGenVarBuckets[] = {4, 8, 12, 16, 0};
+static int gen_bucket(int32_t dmax, const int* buckets)
+{
+    for (const int* b = buckets; *b; ++b)
+        if (dmax <= *b) return *b;
+    return 0;
+}
+
 // `res` the resident pool's in-place check + fused syndrome step (rstep)
 int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt)
 {
@@ -487,10 +499,26 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
             else if (nt_d) klaunch((k_check_bp<72, true, false>), grid, blk, 0, s, v2c, scratch, active, M, E, t0, ResStep{});
             else klaunch((k_check_bp<72, false, false>), grid, blk, 0, s, v2c, scratch, active, M, E, t0, ResStep{});
         });
-    } else if (algo == LDPC_ALGO_BP) {
-        LAUNCH_ON(s, K_CHECK, klaunch(k_check_bp_gen, grid, blk, 0, s, v2c, scratch, active, d_row_ptr, M, E, t0));
     } else {
-        LAUNCH_ON(s, K_CHECK, klaunch(k_check_msa_gen, grid, blk, 0, s, v2c, scratch, active, d_row_ptr, M, E, t0));
+        // generic row degrees: registers up to the bucket of dc_max, else memory
+        const bool bp = algo == LDPC_ALGO_BP;
+#define CHECK_GR(D)                                                                                                 \
+    (bp ? klaunch(k_check_bp_gr<D>, grid, blk, 0, s, v2c, scratch, active, d_row_ptr, M, E, t0)                    \
+        : klaunch(k_check_msa_gr<D>, grid, blk, 0, s, v2c, scratch, active, d_row_ptr, M, E, t0))
+        LAUNCH_ON(s, K_CHECK, {
+            switch (gen_bucket(g->dc_max, kGenCheckBuckets)) {
+                case 8: CHECK_GR(8); break;
+                case 16: CHECK_GR(16); break;
+                case 32: CHECK_GR(32); break;
+                case 48: CHECK_GR(48); break;
+                case 64: CHECK_GR(64); break;
+                case 96: CHECK_GR(96); break;
+                default:
+                    if (bp) klaunch(k_check_bp_gen, grid, blk, 0, s, v2c, scratch, active, d_row_ptr, M, E, t0);
+                    else klaunch(k_check_msa_gen, grid, blk, 0, s, v2c, scratch, active, d_row_ptr, M, E, t0);
+            }
+        });
+#undef CHECK_GR
     }
     return LDPC_OK;
 }
@@ -595,6 +623,24 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
     }
     if (cnt) { set_error("continuous mode needs the regular variable kernels"); return LDPC_ERR_ARG; }
     const dim3 grid((N + 3) / 4, gt), blk(256);
+    // generic column degrees: registers up to the bucket of dv_max, else memory
+    const int vb = gen_bucket(g->dv_max, kGenVarBuckets);
+    if (vb) {
+        const bool bp = algo == LDPC_ALGO_BP;
+#define VAR_GR(D)                                                                                                   \
+    (bp ? klaunch(k_var_bp_gr<D>, grid, blk, 0, s, scratch, v2c, prior, hard, active, d_col_ptr, d_col_edge, pt, N, \
+                  E, t0)                                                                                            \
+        : klaunch(k_var_msa_gr<D>, grid, blk, 0, s, scratch, v2c, prior, hard, active, d_col_ptr, d_col_edge, pt,   \
+                  N, E, t0))
+        LAUNCH_ON(s, K_VAR, {
+            if (vb == 4) VAR_GR(4);
+            else if (vb == 8) VAR_GR(8);
+            else if (vb == 12) VAR_GR(12);
+            else VAR_GR(16);
+        });
+#undef VAR_GR
+        return LDPC_OK;
+    }
     if (algo == LDPC_ALGO_BP)
         LAUNCH_ON(s, K_VAR, klaunch(k_var_bp_gen, grid, blk, 0, s, scratch, v2c, prior, hard, active, d_col_ptr, d_col_edge, pt, N, E, t0));
     else

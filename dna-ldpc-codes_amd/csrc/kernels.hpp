@@ -1063,6 +1063,240 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Generic degrees staged in registers (codes other than the (8, 72)-regular
+// one; fixed passes).  A row / column of degree d <= D keeps its messages in
+// VGPRs: one load and one store per edge, where the *_gen kernels above take
+// their partial products through memory (about 40 B per edge per phase
+// instead of 16).  D is the engine's bucket for the graph's maximum degree
+// (engine.hip kGenBuckets); every loop runs the same operations in the same
+// order as the *_gen kernels (and the reference), guarded by k < d.
+template <int D>
+__device__ __forceinline__ void check_bp_compute_rt(const double (&x)[D], int32_t d, double* __restrict__ dst)
+{
+    constexpr int SEG = 8;
+    constexpr int NSEG = (D + SEG - 1) / SEG;
+    double cp[NSEG];
+    double p = 1.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        if (k < d) {
+            if (k % SEG == 0) cp[k / SEG] = p;
+            p = p * x[k];
+        }
+    }
+    double s = 1.0;
+#pragma unroll
+    for (int g = NSEG - 1; g >= 0; --g) {
+        if (g * SEG >= d) continue;
+        double pk[SEG];
+        double q = cp[g];
+        asm volatile("" : "+v"(q));  // (as check_bp_compute: no CSE with the forward pass)
+#pragma unroll
+        for (int i = 0; i < SEG; ++i) {
+            const int k = g * SEG + i;
+            if (k < D && k < d) { pk[i] = q; q = q * x[k]; }
+        }
+#pragma unroll
+        for (int i = SEG - 1; i >= 0; --i) {
+            const int k = g * SEG + i;
+            if (k < D && k < d) {
+                const double tt = pk[i] * s;
+                dst[(size_t)k * TILE] = (1.0 + tt) / (1.0 - tt);
+                s = s * x[k];
+            }
+        }
+    }
+}
+
+// BP check phase (dec.cpp:646-662), rows of degree <= D in registers
+template <int D>
+__global__ __launch_bounds__(256) void k_check_bp_gr(const double* __restrict__ dmsg, double* __restrict__ lr,
+                                                     const uint64_t* __restrict__ active,
+                                                     const int32_t* __restrict__ row_ptr, int32_t M, int64_t E,
+                                                     int64_t t0)
+{
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = t0 + blockIdx.y;
+    if (row >= M) return;
+    if (!((active[t] >> lane) & 1ull)) return;
+    const int32_t a = row_ptr[row], d = row_ptr[row + 1] - a;
+    const double* src = dmsg + ((size_t)t * E + a) * TILE + lane;
+    double* dst = lr + ((size_t)blockIdx.y * E + a) * TILE + lane;
+    double x[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+        if (k < d) x[k] = src[(size_t)k * TILE];
+    check_bp_compute_rt<D>(x, d, dst);
+}
+
+// min-sum check phase (dec.cpp:1398-1433, as k_check_msa_gen), rows of
+// degree <= D in registers
+template <int D>
+__global__ __launch_bounds__(256) void k_check_msa_gr(const double* __restrict__ v2c, double* __restrict__ c2v,
+                                                      const uint64_t* __restrict__ active,
+                                                      const int32_t* __restrict__ row_ptr, int32_t M, int64_t E,
+                                                      int64_t t0)
+{
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = t0 + blockIdx.y;
+    if (row >= M) return;
+    if (!((active[t] >> lane) & 1ull)) return;
+    const int32_t a = row_ptr[row], d = row_ptr[row + 1] - a;
+    double* dst = c2v + ((size_t)blockIdx.y * E + a) * TILE + lane;
+    if (d == 0) return;
+    if (d == 1) { dst[0] = 0.0; return; }
+    const double* src = v2c + ((size_t)t * E + a) * TILE + lane;
+    double x[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+        if (k < d) x[k] = src[(size_t)k * TILE];
+    double m1 = __builtin_inf(), m2 = __builtin_inf();
+    int32_t i1 = -1;
+    uint32_t neg = 0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        if (k < d) {
+            const double av = __builtin_fabs(x[k]);
+            neg ^= (x[k] >= 0) ? 0u : 1u;
+            if (av < m1) { m1 = av; i1 = k; }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        if (k < d) {
+            const double av = __builtin_fabs(x[k]);
+            if (k != i1 && av < m2) m2 = av;
+        }
+    }
+    const double a0 = __builtin_fabs(x[0]), a1 = __builtin_fabs(x[1]);
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        if (k < d) {
+            const double af = (k == 0) ? a1 : a0;
+            double mag = (k == i1) ? m2 : m1;
+            if (__builtin_isnan(af)) mag = af;
+            const uint32_t nk = (x[k] >= 0) ? 0u : 1u;
+            const int sign = ((neg ^ nk) & 1u) ? -1 : 1;
+            dst[(size_t)k * TILE] = (double)sign * mag;
+        }
+    }
+}
+
+// BP variable phase + decision (dec.cpp:667-693, as k_var_bp_gen), columns
+// of degree <= D in registers
+template <int D>
+__global__ __launch_bounds__(256) void k_var_bp_gr(const double* __restrict__ lr, double* __restrict__ dmsg,
+                                                   const double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                                   const uint64_t* __restrict__ active,
+                                                   const int32_t* __restrict__ col_ptr,
+                                                   const int32_t* __restrict__ col_edge, double* __restrict__ post,
+                                                   int32_t N, int64_t E, int64_t t0)
+{
+    const int lane = lane_id();
+    const int32_t j = blockIdx.x * 4 + wave_id();
+    const int64_t t = t0 + blockIdx.y;
+    if (j >= N) return;
+    const uint64_t act = active[t];
+    if (act == 0) return;
+    const bool live = (act >> lane) & 1ull;
+    const int32_t a = col_ptr[j], d = col_ptr[j + 1] - a;
+    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
+    bool h = false;
+    if (live) {
+        int32_t eid[D];
+        double l[D], pr[D];
+#pragma unroll
+        for (int s = 0; s < D; ++s)
+            if (s < d) eid[s] = col_edge[a + s];
+#pragma unroll
+        for (int s = 0; s < D; ++s)
+            if (s < d) l[s] = lr[(tl + eid[s]) * TILE + lane];
+        const size_t pj = ((size_t)t * N + j) * TILE + lane;
+        double p = prior[pj];
+#pragma unroll
+        for (int s = 0; s < D; ++s)
+            if (s < d) { pr[s] = p; p = p * l[s]; }
+        if (__builtin_isnan(p)) p = 1.0;
+        h = (p <= 1.0);
+        if (post) post[pj] = p;
+        double acc = 1.0;
+#pragma unroll
+        for (int s = D - 1; s >= 0; --s) {
+            if (s < d) {
+                double v = pr[s] * acc;
+                if (__builtin_isnan(v)) v = 1.0;
+                acc = acc * l[s];
+                dmsg[(tb + eid[s]) * TILE + lane] = 1.0 - 2.0 / (1.0 + v);
+            }
+        }
+    }
+    const uint64_t m = __ballot(h);
+    if (lane == 0) {
+        const size_t o = (size_t)t * N + j;
+        const uint64_t old = (act == ~0ull) ? 0ull : hard[o];
+        hard[o] = (old & ~act) | (m & act);
+    }
+}
+
+// min-sum variable phase + decision (dec.cpp:1597-1619, 1659-1678, as
+// k_var_msa_gen), columns of degree <= D in registers
+template <int D>
+__global__ __launch_bounds__(256) void k_var_msa_gr(const double* __restrict__ c2v, double* __restrict__ v2c,
+                                                    const double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                                    const uint64_t* __restrict__ active,
+                                                    const int32_t* __restrict__ col_ptr,
+                                                    const int32_t* __restrict__ col_edge, double* __restrict__ post,
+                                                    int32_t N, int64_t E, int64_t t0)
+{
+    const int lane = lane_id();
+    const int32_t j = blockIdx.x * 4 + wave_id();
+    const int64_t t = t0 + blockIdx.y;
+    if (j >= N) return;
+    const uint64_t act = active[t];
+    if (act == 0) return;
+    const bool live = (act >> lane) & 1ull;
+    const int32_t a = col_ptr[j], d = col_ptr[j + 1] - a;
+    const size_t tb = (size_t)t * E, tl = (size_t)blockIdx.y * E;
+    bool h = false;
+    if (live) {
+        int32_t eid[D];
+        double c[D];
+#pragma unroll
+        for (int s = 0; s < D; ++s)
+            if (s < d) eid[s] = col_edge[a + s];
+#pragma unroll
+        for (int s = 0; s < D; ++s)
+            if (s < d) c[s] = c2v[(tl + eid[s]) * TILE + lane];
+        const size_t pj = ((size_t)t * N + j) * TILE + lane;
+        const double llr = prior[pj];
+#pragma unroll
+        for (int s = 0; s < D; ++s) {
+            if (s < d) {
+                double sum = llr;
+#pragma unroll
+                for (int r = 0; r < D; ++r)
+                    if (r < d && r != s) sum = sum + c[r];
+                v2c[(tb + eid[s]) * TILE + lane] = sum;
+            }
+        }
+        double L = llr;
+#pragma unroll
+        for (int s = 0; s < D; ++s)
+            if (s < d) L = L + c[s];
+        h = !(L > 0);
+        if (post) post[pj] = L;
+    }
+    const uint64_t m = __ballot(h);
+    if (lane == 0) {
+        const size_t o = (size_t)t * N + j;
+        const uint64_t old = (act == ~0ull) ? 0ull : hard[o];
+        hard[o] = (old & ~act) | (m & act);
+    }
+}
+
 // Raw buffer resource over [base, base + bytes) (gfx9 data format, no
 // swizzle, stride 0).  A wave's gathers and scatters then take a
 // wave-uniform byte offset in an SGPR (soffset) and one shared per-lane
