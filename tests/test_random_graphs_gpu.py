@@ -163,3 +163,50 @@ def test_random_regular_schedules_bitexact(gpu, oracle_mod, tmp_path, sch):
                                          post="ratio" if algo == "bp" else "llr", schedule=schedule)
         assert np.array_equal(h2, h) and np.array_equal(it2, it) and np.array_equal(v2, v)
         assert np.array_equal(p2.view(np.uint64), p.view(np.uint64))
+
+
+def _bucket_graph(rng, M, N, dc_max, dv_max):
+    """Row 0 of degree dc_max, column 0 in dv_max rows, every other row of
+    random degree 1..dc_max and no column in more than dv_max rows: the
+    largest degrees sit exactly on (or one past) a register bucket of the
+    generic kernels (engine.hip kGenCheckBuckets / kGenVarBuckets)."""
+    sets = [set() for _ in range(M)]
+    cnt = np.zeros(N, np.int64)
+    for i in range(dv_max):
+        sets[i].add(0)
+    cnt[0] = dv_max
+    for i in range(M):
+        want = dc_max if i == 0 else int(rng.integers(1, dc_max + 1))
+        for j in rng.permutation(np.arange(1, N)):
+            if len(sets[i]) >= want:
+                break
+            if cnt[j] < dv_max:
+                sets[i].add(int(j))
+                cnt[j] += 1
+    rows = [i for i in range(M) for _ in sets[i]]
+    cols = [j for i in range(M) for j in sorted(sets[i])]
+    return rows, cols
+
+
+BUCKETS = [(8, 4), (9, 5), (16, 8), (17, 9), (32, 12), (33, 13), (48, 16), (49, 17), (64, 3), (65, 2), (96, 16),
+           (97, 17)]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("case", range(len(BUCKETS)))
+def test_generic_bucket_edges_bitexact(gpu, oracle_mod, tmp_path, case):
+    """Maximum row / column degrees on and just past each register bucket
+    (and past the last one: the memory-staged fallback), BP and min-sum, a
+    ragged batch with erasures, infinities and a NaN."""
+    dc, dv = BUCKETS[case]
+    rng = np.random.default_rng(500 + case)
+    M, N = max(dv + 3, 20), 300
+    rows, cols = _bucket_graph(rng, M, N, dc, dv)
+    path = tmp_path / f"bucket{case}.pchk"
+    _write_pchk(path, M, N, rows, cols)
+    og = oracle_mod.OracleGraph(str(path))
+    G = gpu.Graph(str(path))
+    assert (G.dc, G.dv) == (dc, dv)
+    llr = _llr(rng, 130, N, "lattice" if case % 2 else "normal")
+    _cmp_nan(G, og, llr, 20)
+    _cmp_nan(G, og, llr, 20, algo="msa")
