@@ -44,7 +44,7 @@ def main():
     a = ap.parse_args()
     import ldpc_amd as L
     print(f"{'code':32s} {'N':>6} {'M':>5} {'E':>7} {'dv':>3} {'dc':>3} {'path':>10} {'cw/s':>10} "
-          f"{'it/cw':>6} {'GB/s':>7} {'frac':>6}", flush=True)
+          f"{'it/cw':>6} {'GB/s':>7} {'frac':>6} {'chk us':>7} {'var us':>7} {'syn us':>7}", flush=True)
     for name, G in codes(L, None):
         N, E = G.N, G.E
         B = max(64, min(a.batch, int(4e9 // (E * 16 + N * 10))))  # a few GB of state at most
@@ -73,10 +73,14 @@ def main():
         ms = sum(st[k]["ms"] / st[k]["sampled"] * st[k]["launches"] for k in ("check", "variable", "syndrome")
                  if st[k]["sampled"]) / 2
         cwi = float(iters.sum())
+
+        def per(k):  # average launch, us
+            return st[k]["ms"] / st[k]["sampled"] * 1e3 if st[k]["sampled"] else 0.0
         gbs = (32.0 * E + 10.0 * N) * cwi / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         path = "72/8" if (G.dc == 72 and G.dv == 8 and G.regular_dc and G.regular_dv) else "generic"
         print(f"{name:32s} {N:>6} {G.M:>5} {E:>7} {G.dv:>3} {G.dc:>3} {path:>10} {B / el:>10.1f} "
-              f"{cwi / B:>6.1f} {gbs:>7.1f} {gbs / 8000:>6.3f}", flush=True)
+              f"{cwi / B:>6.1f} {gbs:>7.1f} {gbs / 8000:>6.3f} {per('check'):>7.1f} {per('variable'):>7.1f} "
+              f"{per('syndrome'):>7.1f}", flush=True)
         for b in (d_cw, d_in, d_h, d_i, d_v):
             b.free()
         eng.close()
