@@ -155,6 +155,19 @@ static uint16_t* msa_meta(double* scratch, int64_t tiles, int32_t M)
     return reinterpret_cast<uint16_t*>(scratch + (size_t)tiles * M * dev::MSA_REC_PLANES * dev::TILE);
 }
 
+// Degree buckets of the register-staged generic kernels (kernels.hpp *_gr):
+// the smallest bucket >= the graph's maximum degree, 0 when none holds it
+// (the memory-staged *_gen kernels then run; no continuous mode without a
+// variable bucket).
+static constexpr int kGenCheckBuckets[] = {8, 16, 32, 48, 64, 96, 0};
+static constexpr int kGenVarBuckets[] = {4, 8, 12, 16, 0};
+static int gen_bucket(int32_t dmax, const int* buckets)
+{
+    for (const int* b = buckets; *b; ++b)
+        if (dmax <= *b) return *b;
+    return 0;
+}
+
 int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, const ldpc_schedule* schedule,
                  bool resolved)
 {
@@ -181,12 +194,16 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     // compressed min-sum: the packed column table carries edge ids (E < 2^18)
     msa_c = algo == LDPC_ALGO_MSA && reg_72_8 && g->N % 16 == 0 && g->E < ((int64_t)1 << dev::MSA_ER_SHIFT) &&
             sched_flag(sched, LDPC_SCHED_MSA_COMPRESSED);
-    cont = sched_flag(sched, LDPC_SCHED_CONTINUOUS) && !int_algo && reg_72_8;
+    // continuous mode: the specialised kernels, or any code whose column
+    // degrees fit a register bucket of the generic continuous variable kernel
+    // (k_var_gr_cont; its syndrome k_syndrome_split_gen)
+    cont = sched_flag(sched, LDPC_SCHED_CONTINUOUS) && !int_algo &&
+           (reg_72_8 || (g->regular_dv && g->dv_max == 8) || gen_bucket(g->dv_max, kGenVarBuckets) != 0);
     // resident pool: a few tiles whose whole state fits the
     // Infinity Cache, check->variable messages written over the variable->check
     // messages they are computed from (each row's / column's edges are read
     // into registers before its outputs are stored), no c2v scratch
-    res = sched_flag(sched, LDPC_SCHED_RESIDENT) && cont && !msa_c && g->N % 32 == 0;
+    res = sched_flag(sched, LDPC_SCHED_RESIDENT) && cont && reg_72_8 && !msa_c && g->N % 32 == 0;
     // by default the resident pool is the Infinity-Cache-sized one: a caller's
     // explicit larger pool (the host API's chunks, the DNA batch) runs the
     // grouped schedule (A/B, 272-codeword DNA batch at cap 320: 193k -> 250k cw/s)
@@ -275,7 +292,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         syn_blocks = res ? 0 : sched.syn_blocks;
         // single fill (the DNA batch): step 0's refill stores only the prior and
         // step 1's check derives the first messages from it (k_check_bp_first)
-        first_fp = !res && algo == LDPC_ALGO_BP && sched_flag(sched, LDPC_SCHED_FIRST_FROM_PRIOR);
+        first_fp = !res && reg_72_8 && algo == LDPC_ALGO_BP && sched_flag(sched, LDPC_SCHED_FIRST_FROM_PRIOR);
     }
     const size_t E = (size_t)std::max<int64_t>(g->E, 1);
     LDPC_HIP(hipMalloc((void**)&v2c, (size_t)cap * E * sizeof(double)));
@@ -452,18 +469,6 @@ int Engine::collect_stats()
 #define LAUNCH(cls, ...) LAUNCH_ON(stream, cls, __VA_ARGS__)
 
 // check phase of tiles t0 .. t0+gt-1 into `scratch` (that group's c2v); with
-// Degree buckets of the register-staged generic kernels (kernels.hpp *_gr):
-// the smallest bucket >= the graph's maximum degree, 0 when none holds it
-// (the memory-staged *_gen kernels then run).
-static constexpr int kGenCheckBuckets[] = {8, 16, 32, 48, 64, 96, 0};
-static constexpr int kGenVarBuckets[] = {4, 8, 12, 16, 0};
-static int gen_bucket(int32_t dmax, const int* buckets)
-{
-    for (const int* b = buckets; *b; ++b)
-        if (dmax <= *b) return *b;
-    return 0;
-}
-
 // `res` the resident pool's in-place check + fused syndrome step (rstep)
 int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt)
 {
@@ -621,10 +626,32 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         });
         return LDPC_OK;
     }
-    if (cnt) { set_error("continuous mode needs the regular variable kernels"); return LDPC_ERR_ARG; }
     const dim3 grid((N + 3) / 4, gt), blk(256);
     // generic column degrees: registers up to the bucket of dv_max, else memory
     const int vb = gen_bucket(g->dv_max, kGenVarBuckets);
+    if (cnt) {
+        if (!vb) { set_error("continuous mode needs column degrees <= 16"); return LDPC_ERR_ARG; }
+        const bool pc = rf.in_code != nullptr;
+#define VAR_GRC2(MSA, D)                                                                                             \
+    (pc ? klaunch((k_var_gr_cont<MSA, D, true>), grid, blk, 0, s, scratch, v2c, prior, hard, active, d_col_ptr,     \
+                  d_col_edge, pt, N, E, t0, rf)                                                                      \
+        : klaunch((k_var_gr_cont<MSA, D, false>), grid, blk, 0, s, scratch, v2c, prior, hard, active, d_col_ptr,    \
+                  d_col_edge, pt, N, E, t0, rf))
+#define VAR_GRC(D)                          \
+    do {                                    \
+        if (algo == LDPC_ALGO_MSA) VAR_GRC2(true, D); \
+        else VAR_GRC2(false, D);            \
+    } while (0)
+        LAUNCH_ON(s, K_VAR, {
+            if (vb == 4) VAR_GRC(4);
+            else if (vb == 8) VAR_GRC(8);
+            else if (vb == 12) VAR_GRC(12);
+            else VAR_GRC(16);
+        });
+#undef VAR_GRC
+#undef VAR_GRC2
+        return LDPC_OK;
+    }
     if (vb) {
         const bool bp = algo == LDPC_ALGO_BP;
 #define VAR_GR(D)                                                                                                   \
@@ -995,7 +1022,9 @@ int Engine::run_cont_steps(const double* d_in, int in_kind, int64_t B, int32_t m
     cs.fault = d_fault;
     cs.debug_bad_lane = debug_bad_lane ? 1 : 0;
     const uint64_t q0 = poll_seq;  // this decode's first poll
-    ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, ContOut{d_iters, d_valid}};
+    ResStep rs{hard, d_col_idx, d_unsat, d_done, d_fin, d_fin_b, d_fin_n, N, max_iter, cs, ContOut{d_iters, d_valid},
+               d_row_ptr};
+    const bool syn72 = g->regular_dc && g->dc_max == 72;
     const int hard_vec = ((uintptr_t)d_hard % 8 == 0 && N % 8 == 0) ? 1 : 0;
     Refill rf{d_fresh, d_lane_b, d_in, in_kind == LDPC_IN_LLR ? 1 : 0, d_fin, d_fin_b, d_fin_n,
               d_hard, d_post, post_kind == LDPC_POST_RATIO ? 1 : 0, hard_vec};
@@ -1082,8 +1111,12 @@ int Engine::run_cont_steps(const double* d_in, int in_kind, int64_t B, int32_t m
         if (s >= limit) return overrun(s);
         const uint64_t q = poll_seq++;
         poll_arm(rs.cs, q);
-        LAUNCH(K_SYN, klaunch(k_syndrome_split<72>, dim3((unsigned)(syn_blocks * tiles)), dim3(256), 0, stream, M,
-                              rs, (uint32_t)tiles));
+        if (syn72)
+            LAUNCH(K_SYN, klaunch(k_syndrome_split<72>, dim3((unsigned)(syn_blocks * tiles)), dim3(256), 0, stream,
+                                  M, rs, (uint32_t)tiles));
+        else
+            LAUNCH(K_SYN, klaunch(k_syndrome_split_gen, dim3((unsigned)(syn_blocks * tiles)), dim3(256), 0, stream,
+                                  M, rs, (uint32_t)tiles));
         const int64_t gstep = low ? std::max(group_tiles, c2v_tiles) : group_tiles;
         if (ffp && cur_codes && s == 0 && N % 64 == 0) {
             // single fill on codes: step 0 is the transpose of the claimed

@@ -106,6 +106,7 @@ struct ResStep {
     int32_t N, max_iter;
     ContState cs;
     ContOut co;                  // iters / valid (hard / post are written by the variable kernel)
+    const int32_t* row_ptr = nullptr;  // [M+1] CSR row starts (k_syndrome_split_gen: any row degrees)
 };
 
 }  // namespace dev

@@ -1297,6 +1297,160 @@ __global__ __launch_bounds__(256) void k_var_msa_gr(const double* __restrict__ c
     }
 }
 
+// Continuous mode for column degrees <= D (codes other than the
+// (8, 72)-regular one): var_m_block's lane handling -- finished lanes' outputs
+// first, refilled lanes' Init_Belief_Propagation (dec.cpp:608-629) /
+// Init_MSA_INF (dec.cpp:1300-1329), live lanes' update as k_var_bp_gr /
+// k_var_msa_gr -- for one column per wave with the degree read from col_ptr.
+// PC: coded priors (Refill::pcode / ptab, refills from Refill::in_code).
+template <bool MSA, int D, bool PC>
+__global__ __launch_bounds__(256) void k_var_gr_cont(const double* __restrict__ c2v, double* __restrict__ v2c,
+                                                     double* __restrict__ prior, uint64_t* __restrict__ hard,
+                                                     const uint64_t* __restrict__ active,
+                                                     const int32_t* __restrict__ col_ptr,
+                                                     const int32_t* __restrict__ col_edge, double* __restrict__ post,
+                                                     int32_t N, int64_t E, int64_t t0, Refill rf)
+{
+    const int lane = lane_id();
+    const int32_t j = blockIdx.x * 4 + wave_id();
+    const int64_t t = t0 + blockIdx.y;
+    if (j >= N) return;
+    const uint64_t act = active[t];
+    const uint64_t frm = rf.fresh[t];
+    const uint64_t touched = act | frm;
+    const uint64_t fm = rf.fin ? rf.fin[t] : 0ull;
+    if (touched == 0 && fm == 0) return;
+    const bool live = (act >> lane) & 1ull;
+    const bool fr = (frm >> lane) & 1ull;
+    const bool fl = (fm >> lane) & 1ull;
+    int64_t fb = 0;
+    int32_t fn = 0;
+    if (fl) {
+        fb = rf.fin_b[t * TILE + lane];
+        fn = rf.fin_n[t * TILE + lane];
+    }
+    const int32_t a = col_ptr[j], d = col_ptr[j + 1] - a;
+    const size_t tb = (size_t)t * E;
+    const double* __restrict__ c2v_t = c2v + (size_t)blockIdx.y * E * TILE;
+    int32_t eid[D];
+#pragma unroll
+    for (int s = 0; s < D; ++s)
+        if (s < d) eid[s] = col_edge[a + s];
+    bool bad_in = false;
+    int bad_v = 0;
+    double xin = 0.0;
+    int8_t kin = 0;
+    if (fr) {  // refilled lane: its input value, loaded with the c2v loads
+        const size_t rb = (size_t)refill_row(rf.lane_b[t * TILE + lane], rf, bad_in) * N;
+        bad_v = bad_in ? 1 : 0;
+        if constexpr (PC) kin = rf.in_code[rb + j];
+        else xin = rf.in[rb + j];
+    }
+    const size_t pj = ((size_t)t * N + j) * TILE + lane;
+    double l[D];
+    double pv = 0.0;
+    if (live) {
+        pv = prior_at<PC>(prior, rf, pj);
+#pragma unroll
+        for (int s = 0; s < D; ++s)
+            if (s < d) l[s] = c2v_t[(size_t)eid[s] * TILE + lane];
+    }
+    if constexpr (PC) {
+        if (fr) xin = rf.ptab[kin + kCodeBias];
+    }
+    const bool fok = out_ok(fb, rf);
+    if (fl && fok) {  // finished codeword: hard bits of its exit (ballots before this step's update)
+        const uint64_t hw[1] = {hard[(size_t)t * N + j]};
+        store_fin_hard<1>(rf, hw, fb, N, j, lane);
+        if (rf.post_out) {  // and its posterior
+            const double q = fn > 0 ? post[pj] : prior_at<PC>(prior, rf, pj);
+            if (MSA) rf.post_out[(size_t)fb * N + j] = q;
+            else {
+                const double P = __builtin_isnan(q) ? 1.0 : q;
+                rf.post_out[(size_t)fb * N + j] = rf.post_ratio ? P : log(P);
+            }
+        }
+    }
+    bool h = false;
+    double dv[D];
+#pragma unroll
+    for (int s = 0; s < D; ++s) dv[s] = 0.0;
+    double np = live ? pv : 0.0;
+    if (fr) {
+        const double x = xin;
+        if (MSA) {
+            np = x;
+#pragma unroll
+            for (int s = 0; s < D; ++s) dv[s] = x;
+            h = !(x > 0);
+        } else {
+            const double LR0 = (!PC && rf.in_is_llr) ? exp(x) : x;
+            np = LR0;
+            const double d0 = 1.0 - 2.0 / (1.0 + LR0);
+#pragma unroll
+            for (int s = 0; s < D; ++s) dv[s] = d0;
+            h = (LR0 < 1.0);
+        }
+    } else if (live) {
+        if (MSA) {
+#pragma unroll
+            for (int s = 0; s < D; ++s) {
+                if (s < d) {
+                    double sum = pv;
+#pragma unroll
+                    for (int r = 0; r < D; ++r)
+                        if (r < d && r != s) sum = sum + l[r];
+                    dv[s] = sum;
+                }
+            }
+            double L = pv;
+#pragma unroll
+            for (int s = 0; s < D; ++s)
+                if (s < d) L = L + l[s];
+            h = !(L > 0);
+            if (post) post[pj] = L;
+        } else {
+            double pr[D];
+            double p = pv;
+#pragma unroll
+            for (int s = 0; s < D; ++s)
+                if (s < d) { pr[s] = p; p = p * l[s]; }
+            if (__builtin_isnan(p)) p = 1.0;
+            h = (p <= 1.0);
+            if (post) post[pj] = p;
+            double acc = 1.0;
+#pragma unroll
+            for (int s = D - 1; s >= 0; --s) {
+                if (s < d) {
+                    double v = pr[s] * acc;
+                    if (__builtin_isnan(v)) v = 1.0;
+                    acc = acc * l[s];
+                    dv[s] = 1.0 - 2.0 / (1.0 + v);
+                }
+            }
+        }
+    }
+    if (fr) {
+        if constexpr (PC) rf.pcode[pj] = kin;
+        else prior[pj] = np;
+    }
+    // whole-line stores, as var_m_block (others write 0, never read)
+    if (line_occupied(touched, lane) || fr || live) {
+#pragma unroll
+        for (int s = 0; s < D; ++s)
+            if (s < d) v2c[(tb + eid[s]) * TILE + lane] = dv[s];
+    }
+    const uint64_t m = __ballot(h);
+    if (lane == 0 && touched) {
+        const size_t o = (size_t)t * N + j;
+        const uint64_t old = (touched == ~0ull) ? 0ull : hard[o];
+        hard[o] = (old & ~touched) | (m & touched);
+    }
+    if (fl && !fok) lane_fault(rf.fault, kFaultOutput, t * TILE + lane);
+    asm volatile("" : "+v"(bad_v));
+    if (bad_v) lane_fault(rf.fault, kFaultRefill, t * TILE + lane);
+}
+
 // Raw buffer resource over [base, base + bytes) (gfx9 data format, no
 // swizzle, stride 0).  A wave's gathers and scatters then take a
 // wave-uniform byte offset in an SGPR (soffset) and one shared per-lane
@@ -1737,6 +1891,46 @@ __global__ __launch_bounds__(256) void k_syndrome_split(int32_t M, ResStep rs, u
                     const int k = part * KP + q;
                     if (k < DC) p ^= h[cols[k]];
                 }
+            }
+            p ^= shfl_xor_u64(p, 8);
+            p ^= shfl_xor_u64(p, 16);
+            p ^= shfl_xor_u64(p, 32);
+            u |= p;
+        }
+        u |= shfl_xor_u64(u, 1);
+        u |= shfl_xor_u64(u, 2);
+        u |= shfl_xor_u64(u, 4);
+    }
+    res_arrive(t, occ, u, rs, ln0, b0, nblk);
+}
+
+// k_syndrome_split for any row degrees (codes other than the regular
+// degree-72 one, continuous mode): lane (part, row) XORs the ballots of edges
+// part*KP .. part*KP+KP-1 of its row, KP = ceil(d / 8) of that row's degree d.
+__global__ __launch_bounds__(256) void k_syndrome_split_gen(int32_t M, ResStep rs, uint32_t tiles)
+{
+    const int64_t t = blockIdx.x % tiles;
+    const uint32_t blk = blockIdx.x / tiles, nblk = gridDim.x / tiles;
+    const uint64_t occ = rs.cs.occupied[t];
+    const int lane = lane_id();
+    int32_t ln0 = 0;
+    int64_t b0 = 0;
+    uint64_t u = 0;
+    if (occ) {
+        if (threadIdx.x < TILE && ((occ >> lane) & 1ull)) {
+            ln0 = rs.cs.lane_n[t * TILE + lane];
+            b0 = rs.cs.lane_b[t * TILE + lane];
+        }
+        const uint64_t* __restrict__ h = rs.hard + (size_t)t * rs.N;
+        const int part = lane >> 3;
+        for (int32_t r0 = (int32_t)(blk * 4 + wave_id()) * 8; r0 < M; r0 += (int32_t)nblk * 32) {
+            const int32_t row = r0 + (lane & 7);
+            uint64_t p = 0;
+            if (row < M) {
+                const int32_t a = rs.row_ptr[row], b = rs.row_ptr[row + 1];
+                const int32_t kp = (b - a + 7) / 8;
+                const int32_t e0 = a + part * kp, e1 = e0 + kp < b ? e0 + kp : b;
+                for (int32_t e = e0; e < e1; ++e) p ^= h[rs.col_idx[e]];
             }
             p ^= shfl_xor_u64(p, 8);
             p ^= shfl_xor_u64(p, 16);

@@ -17,13 +17,14 @@ from test_gpu_parity import _cmp, _write_pchk
 pytestmark = pytest.mark.gpu
 
 
-def _cmp_nan(G, og, llr, max_iter, algo="bp"):
+def _cmp_nan(G, og, llr, max_iter, algo="bp", schedule=None):
     """test_gpu_parity._cmp, with the NaN rule of test_nan_and_infinite_llrs:
     a NaN posterior only has to be matched by a NaN (payload and sign are not
     part of the contract); everything else bit for bit."""
     a = 0 if algo == "bp" else 1
     ref_h, ref_p, ref_it, ref_v = og.decode_batch(llr, max_iter, algo=a, post_mode=1 if a == 0 else 0, threads=8)
-    h, p, it, v = G.decode(llr, max_iter=max_iter, algo=algo, post="ratio" if a == 0 else "llr")
+    kw = {"schedule": schedule} if schedule else {}
+    h, p, it, v = G.decode(llr, max_iter=max_iter, algo=algo, post="ratio" if a == 0 else "llr", **kw)
     assert np.array_equal(it, ref_it) and np.array_equal(v, ref_v.astype(bool)) and np.array_equal(h, ref_h), algo
     nan = np.isnan(ref_p)
     assert np.array_equal(np.isnan(p), nan), algo
@@ -100,8 +101,9 @@ def test_random_graph_bitexact(gpu, oracle_mod, tmp_path, case):
     G = gpu.Graph(str(path))
     assert (G.M, G.N, G.E) == (og.M, og.N, og.E)
     llr = _llr(rng, B, N, kind)
-    _cmp_nan(G, og, llr, max_iter)
-    _cmp_nan(G, og, llr, max_iter, algo="msa")
+    for sch in (None, {"continuous": False}):  # continuous lane pool (column degree <= 16), fixed passes
+        _cmp_nan(G, og, llr, max_iter, schedule=sch)
+        _cmp_nan(G, og, llr, max_iter, algo="msa", schedule=sch)
     if case % 3 == 0:  # the integer decoders: Gallager A / B1 / B2 and quantized min-sum
         for algo, name in ((3, "gallager_a"), (4, "gallager_b1"), (5, "gallager_b2"), (2, "qmsa")):
             rh, _, rit, rv = og.decode_int_batch(llr, max_iter, algo)
@@ -208,5 +210,51 @@ def test_generic_bucket_edges_bitexact(gpu, oracle_mod, tmp_path, case):
     G = gpu.Graph(str(path))
     assert (G.dc, G.dv) == (dc, dv)
     llr = _llr(rng, 130, N, "lattice" if case % 2 else "normal")
-    _cmp_nan(G, og, llr, 20)
-    _cmp_nan(G, og, llr, 20, algo="msa")
+    for sch in (None, {"continuous": False}):
+        _cmp_nan(G, og, llr, 20, schedule=sch)
+        _cmp_nan(G, og, llr, 20, algo="msa", schedule=sch)
+
+
+GEN_SCHEDULES = [{}, {"continuous": False}, {"group_tiles": 1}, {"syn_blocks": 1}, {"syn_blocks": 64, "group_tiles": 2}]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("sch", range(len(GEN_SCHEDULES)))
+def test_generic_continuous_bitexact(gpu, oracle_mod, tmp_path, sch):
+    """Codes other than the (8, 72)-regular one in the continuous lane pool
+    (k_var_gr_cont, k_syndrome_split_gen): an RS-LDPC code (RS_LDPC.c) and an
+    irregular random code, early-exiting BSC words in a batch several times
+    the pool (lanes refilled as codewords finish), fp64 and int8-coded input,
+    posteriors of every finished codeword -- equal to the oracle, and to the
+    fixed-pass schedule."""
+    rng = np.random.default_rng(900 + sch)
+    schedule = GEN_SCHEDULES[sch]
+    rows, cols = _random_graph(rng, 90, 700, 4, 40)
+    path = tmp_path / "irr.pchk"
+    _write_pchk(path, 90, 700, rows, cols)
+    graphs = [gpu.Graph.rs_ldpc(6, 32, 4), gpu.Graph(str(path))]
+    ogs = [None, oracle_mod.OracleGraph(str(path))]
+    rs_path = tmp_path / "rs.pchk"
+    graphs[0].save_pchk(str(rs_path))
+    ogs[0] = oracle_mod.OracleGraph(str(rs_path))
+    unit = 3.8918202981106265
+    table = np.arange(-128, 128, dtype=np.float64) * unit
+    for G, og in zip(graphs, ogs):
+        assert G.dv <= 16 and not (G.dc == 72 and G.dv == 8)
+        B = 1000
+        for algo, p in (("bp", 0.01), ("msa", 0.003)):
+            codes = np.where(rng.random((B, G.N)) < p, -1, 1).astype(np.int8)
+            codes[rng.random((B, G.N)) < 0.01] = 0
+            codes[rng.random((B, G.N)) < 0.002] = 3
+            llr = np.ascontiguousarray(table[codes.astype(np.int64) + 128])
+            a = 0 if algo == "bp" else 1
+            post = "ratio" if a == 0 else "llr"
+            rh, rp, rit, rv = og.decode_batch(llr, 30, algo=a, post_mode=1 if a == 0 else 0, threads=8)
+            eng_kw = dict(max_iter=30, algo=algo, post=post, schedule=schedule, chunk=256)
+            h, pp, it, v = G.decode(llr, **eng_kw)
+            assert np.array_equal(h, rh) and np.array_equal(it, rit) and np.array_equal(v, rv.astype(bool)), algo
+            assert np.array_equal(pp.view(np.uint64), rp.view(np.uint64)), algo
+            h2, p2, it2, v2 = G.decode_codes(codes, table, **eng_kw)
+            assert np.array_equal(h2, h) and np.array_equal(it2, it) and np.array_equal(v2, v), algo
+            assert np.array_equal(p2.view(np.uint64), pp.view(np.uint64)), algo
+            assert 1 < it.mean() < 30  # early exits: the pool refills

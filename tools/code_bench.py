@@ -41,14 +41,21 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--algo", default="bp")
     ap.add_argument("--p", type=float, default=0.05)
+    ap.add_argument("--chunk", type=int, default=0, help="lane pool / pass size (default: the batch)")
+    ap.add_argument("--fixed", action="store_true", help="fixed passes instead of the continuous lane pool")
+    ap.add_argument("--only", default="", help="substring of the code names to run")
     a = ap.parse_args()
     import ldpc_amd as L
     print(f"{'code':32s} {'N':>6} {'M':>5} {'E':>7} {'dv':>3} {'dc':>3} {'path':>10} {'cw/s':>10} "
           f"{'it/cw':>6} {'GB/s':>7} {'frac':>6} {'chk us':>7} {'var us':>7} {'syn us':>7}", flush=True)
     for name, G in codes(L, None):
+        if a.only and a.only not in name:
+            continue
         N, E = G.N, G.E
-        B = max(64, min(a.batch, int(4e9 // (E * 16 + N * 10))))  # a few GB of state at most
-        eng = L.Engine(G, 0, a.algo, chunk=B)
+        # a few GB of state at most (with --chunk the state is the pool's; the batch as given)
+        B = a.batch if a.chunk > 0 else max(64, min(a.batch, int(4e9 // (E * 16 + N * 10))))
+        kw = {"continuous": False} if a.fixed else {}
+        eng = L.Engine(G, 0, a.algo, chunk=min(B, a.chunk) if a.chunk > 0 else B, **kw)
         cw = np.zeros((1, N), np.uint8)
         d_cw = L.DeviceBuffer(0, N)
         d_cw.upload(cw)
