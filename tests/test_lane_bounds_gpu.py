@@ -50,6 +50,34 @@ def test_bad_lane_index_is_reported_not_written(gpu, og, codewords, algo, sch):
 
 
 @pytest.mark.timeout(120)
+@pytest.mark.parametrize("algo", ["bp", "msa"])
+def test_bad_lane_index_generic_code(gpu, oracle_mod, tmp_path, algo):
+    """A code other than the (8, 72)-regular one in the continuous pool
+    (k_syndrome_split_gen's bookkeeping, k_var_gr_cont's guarded refill and
+    output accesses), fp64 and coded input."""
+    L = gpu
+    G2 = L.Graph.rs_ldpc(6, 32, 4)
+    path = tmp_path / "rs.pchk"
+    G2.save_pchk(str(path))
+    og2 = oracle_mod.OracleGraph(str(path))
+    rng = np.random.default_rng(11)
+    B = 700
+    codes = np.where(rng.random((B, G2.N)) < 0.004, -1, 1).astype(np.int8)
+    table = np.arange(-128, 128, dtype=np.float64) * synth.LLR_UNIT
+    llr = np.ascontiguousarray(table[codes.astype(np.int64) + 128])
+    for run in (lambda sch: G2.decode(llr, max_iter=8, algo=algo, post="llr", chunk=256, schedule=sch),
+                lambda sch: G2.decode_codes(codes, table, max_iter=8, algo=algo, post="llr", chunk=256,
+                                            schedule=sch)):
+        with pytest.raises(L.LdpcError) as e:
+            run({"debug_bad_lane": True})
+        assert e.value.code == L.LDPC_ERR_DEVICE, str(e.value)
+        _fault_message(str(e.value), B)
+        h, _, it, v = run({})
+        rh, _, rit, rv = og2.decode_batch(llr, 8, algo=0 if algo == "bp" else 1, threads=8, want_post=False)
+        assert np.array_equal(h, rh) and np.array_equal(it, rit) and np.array_equal(v, rv.astype(bool))
+
+
+@pytest.mark.timeout(120)
 def test_bad_lane_index_single_fill_codes(gpu, og, codewords):
     """The DNA batch's path: one fill of the lane pool from int8 codes, whose
     step 0 is k_fill_codes' transpose of the claimed rows."""
