@@ -74,7 +74,7 @@ ldpc_schedule resolve_schedule(const ldpc_schedule* s)
     // (3: compressed min-sum only; the fp64 variable kernels take 1, 2, 4 or
     // 8); -2: the default, chosen per decode by the prior's form (var_cpw_for)
     if (r.var_cpw < 1 || r.var_cpw > 8 || (r.var_cpw > 4 && r.var_cpw != 8)) r.var_cpw = -2;
-    if (r.pool_tiles <= 0) r.pool_tiles = kDefaultPoolTiles;
+    if (r.pool_tiles <= 0) r.pool_tiles = 0;  // the default, resolved at init (kDefaultPoolTiles / gen_pool_tiles)
     if (r.poll_every <= 0) r.poll_every = kDefaultResPoll;
     if (r.syn_blocks <= 0) r.syn_blocks = kDefaultSynBlocks;
     r.syn_blocks = std::min(r.syn_blocks, 256);
@@ -168,6 +168,16 @@ static int gen_bucket(int32_t dmax, const int* buckets)
     return 0;
 }
 
+// Default resident pool of a code other than the (8, 72)-regular one: as many
+// tiles as keep the pool's messages + fp64 priors within the DNA pool's
+// footprint (kDefaultPoolTiles x 85 MB ~ the 256 MB Infinity Cache).
+constexpr double kGenPoolBytes = 226e6;
+static int32_t gen_pool_tiles(const HostGraph& g)
+{
+    const double per_tile = 64.0 * 8.0 * ((double)g.E + (double)g.N);
+    return (int32_t)std::max(1.0, std::min(256.0, std::floor(kGenPoolBytes / std::max(per_tile, 1.0))));
+}
+
 int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, const ldpc_schedule* schedule,
                  bool resolved)
 {
@@ -176,7 +186,7 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     algo = algorithm;
     if (resolved && schedule && (schedule->flags_set & kResolved)) {
         sched = *schedule;  // the host API's slot: resolved once per call (capi.cpp)
-        sched.pool_tiles = std::max(sched.pool_tiles, 1);
+        sched.pool_tiles = std::max(sched.pool_tiles, 0);
         sched.poll_every = std::max(sched.poll_every, 1);
         sched.syn_blocks = std::min(std::max(sched.syn_blocks, 1), 256);
     } else {
@@ -203,7 +213,10 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     // Infinity Cache, check->variable messages written over the variable->check
     // messages they are computed from (each row's / column's edges are read
     // into registers before its outputs are stored), no c2v scratch
-    res = sched_flag(sched, LDPC_SCHED_RESIDENT) && cont && reg_72_8 && !msa_c && g->N % 32 == 0;
+    // (other codes: row and column degrees in register buckets, k_check_gr_res + k_var_gr_cont in place)
+    const bool gen_res = !reg_72_8 && gen_bucket(g->dc_max, kGenCheckBuckets) != 0 &&
+                         gen_bucket(g->dv_max, kGenVarBuckets) != 0;
+    res = sched_flag(sched, LDPC_SCHED_RESIDENT) && cont && !msa_c && ((reg_72_8 && g->N % 32 == 0) || gen_res);
     // by default the resident pool is the Infinity-Cache-sized one: a caller's
     // explicit larger pool (the host API's chunks, the DNA batch) runs the
     // grouped schedule (A/B, 272-codeword DNA batch at cap 320: 193k -> 250k cw/s)
@@ -220,7 +233,8 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
         // half of the free memory for the resident state, at most 16384 codewords;
         // compressed min-sum in continuous mode: a small lane pool (its scattered
         // v2c stores run ~45 % longer over a 19 GB pool than over 1.2 GB, A/B)
-        const int64_t want = res ? 64 * (int64_t)sched.pool_tiles : (msa_c && cont) ? kMsaPool : 16384;
+        const int64_t ptiles = sched.pool_tiles > 0 ? sched.pool_tiles : reg_72_8 ? kDefaultPoolTiles : gen_pool_tiles(*g);
+        const int64_t want = res ? 64 * ptiles : (msa_c && cont) ? kMsaPool : 16384;
         chunk = std::min<int64_t>(want, (int64_t)(fr / 2) / engine_bytes_per_codeword(*g));
     }
     cap = std::max<int64_t>(64, (chunk + 63) / 64 * 64);
@@ -478,8 +492,25 @@ int Engine::launch_check(hipStream_t s, double* scratch, int64_t t0, unsigned gt
     const bool reg72 = g->regular_dc && g->dc_max == 72;
     const dim3 grid((M + 3) / 4, gt), blk(256);
     const int msa = algo == LDPC_ALGO_MSA;
+    if (res && !reg72) {
+        if (!rstep || scratch != v2c || t0 != 0) { set_error("resident check: bad state"); return LDPC_ERR_ARG; }
+#define CHECK_RES(D)                                                                                            \
+    (msa ? klaunch((k_check_gr_res<true, D>), grid, blk, 0, s, v2c, d_row_ptr, M, E, *rstep)                   \
+         : klaunch((k_check_gr_res<false, D>), grid, blk, 0, s, v2c, d_row_ptr, M, E, *rstep))
+        const int cb = gen_bucket(g->dc_max, kGenCheckBuckets);
+        LAUNCH_ON(s, K_CHECK, {
+            if (cb == 8) CHECK_RES(8);
+            else if (cb == 16) CHECK_RES(16);
+            else if (cb == 32) CHECK_RES(32);
+            else if (cb == 48) CHECK_RES(48);
+            else if (cb == 64) CHECK_RES(64);
+            else CHECK_RES(96);
+        });
+#undef CHECK_RES
+        return LDPC_OK;
+    }
     if (res) {
-        if (!rstep || msa_c || !reg72 || scratch != v2c) { set_error("resident check: bad state"); return LDPC_ERR_ARG; }
+        if (!rstep || msa_c || scratch != v2c) { set_error("resident check: bad state"); return LDPC_ERR_ARG; }
         if (msa)
             LAUNCH_ON(s, K_CHECK, klaunch((k_check_msa<72, false, true>), grid, blk, 0, s, v2c, v2c, active, M, E, t0, *rstep));
         else
@@ -632,11 +663,13 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
     if (cnt) {
         if (!vb) { set_error("continuous mode needs column degrees <= 16"); return LDPC_ERR_ARG; }
         const bool pc = rf.in_code != nullptr;
-#define VAR_GRC2(MSA, D)                                                                                             \
-    (pc ? klaunch((k_var_gr_cont<MSA, D, true>), grid, blk, 0, s, scratch, v2c, prior, hard, active, d_col_ptr,     \
-                  d_col_edge, pt, N, E, t0, rf)                                                                      \
-        : klaunch((k_var_gr_cont<MSA, D, false>), grid, blk, 0, s, scratch, v2c, prior, hard, active, d_col_ptr,    \
-                  d_col_edge, pt, N, E, t0, rf))
+        const bool inplace = scratch == v2c;  // the resident pool
+#define VAR_GRC3(MSA, D, PC)                                                                                         \
+    (inplace ? klaunch((k_var_gr_cont<MSA, D, PC, true>), grid, blk, 0, s, scratch, v2c, prior, hard, active,       \
+                       d_col_ptr, d_col_edge, pt, N, E, t0, rf)                                                      \
+             : klaunch((k_var_gr_cont<MSA, D, PC, false>), grid, blk, 0, s, scratch, v2c, prior, hard, active,      \
+                       d_col_ptr, d_col_edge, pt, N, E, t0, rf))
+#define VAR_GRC2(MSA, D) (pc ? VAR_GRC3(MSA, D, true) : VAR_GRC3(MSA, D, false))
 #define VAR_GRC(D)                          \
     do {                                    \
         if (algo == LDPC_ALGO_MSA) VAR_GRC2(true, D); \
@@ -650,6 +683,7 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
         });
 #undef VAR_GRC
 #undef VAR_GRC2
+#undef VAR_GRC3
         return LDPC_OK;
     }
     if (vb) {

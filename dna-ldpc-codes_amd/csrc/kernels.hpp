@@ -1071,8 +1071,8 @@ __global__ __launch_bounds__(256) void k_var_msa_gen(const double* __restrict__ 
 // instead of 16).  D is the engine's bucket for the graph's maximum degree
 // (engine.hip kGenBuckets); every loop runs the same operations in the same
 // order as the *_gen kernels (and the reference), guarded by k < d.
-template <int D>
-__device__ __forceinline__ void check_bp_compute_rt(const double (&x)[D], int32_t d, double* __restrict__ dst)
+template <int D, bool INPLACE = false>
+__device__ __forceinline__ void check_bp_compute_rt(const double (&x)[D], int32_t d, typename Msg<INPLACE>::out dst)
 {
     constexpr int SEG = 8;
     constexpr int NSEG = (D + SEG - 1) / SEG;
@@ -1297,14 +1297,99 @@ __global__ __launch_bounds__(256) void k_var_msa_gr(const double* __restrict__ c
     }
 }
 
+// Resident pool for row degrees <= D (codes other than the (8, 72)-regular
+// one): k_check_bp_gr / k_check_msa_gr in place over the pool tile
+// blockIdx.y, plus the fused syndrome of the previous variable phase (the
+// row's parity over its ballots, CSR row_ptr / col_idx) and the tile's lane
+// bookkeeping by its last block (res_arrive), as k_check_bp<72, ., true>.
+// Every lane of an occupied 16-lane line runs (whole-line stores); no early
+// return (res_arrive synchronises the block).
+template <bool MSA, int D>
+__global__ __launch_bounds__(256) void k_check_gr_res(double* msg, const int32_t* __restrict__ row_ptr, int32_t M,
+                                                      int64_t E, ResStep rs)
+{
+    const int lane = lane_id();
+    const int32_t row = blockIdx.x * 4 + wave_id();
+    const int64_t t = blockIdx.y;
+    const uint64_t act = rs.cs.occupied[t];
+    uint64_t par = 0;
+    int32_t ln0 = 0;
+    int64_t b0 = 0;
+    int32_t a = 0, d = 0;
+    if (row < M) {
+        a = row_ptr[row];
+        d = row_ptr[row + 1] - a;
+    }
+    if (act != 0) {
+        if (threadIdx.x < TILE && ((act >> lane) & 1ull)) {
+            ln0 = rs.cs.lane_n[t * TILE + lane];
+            b0 = rs.cs.lane_b[t * TILE + lane];
+        }
+        if (row < M) {
+            const uint64_t* __restrict__ h = rs.hard + (size_t)t * rs.N;
+            for (int32_t k0 = 0; k0 < d; k0 += TILE)
+                if (k0 + lane < d) par ^= h[rs.col_idx[a + k0 + lane]];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) par ^= shfl_xor_u64(par, off);
+        }
+    }
+    if (row < M && line_occupied(act, lane) && d > 0) {
+        double* p = msg + ((size_t)t * E + a) * TILE + lane;
+        if (MSA && d == 1) {
+            p[0] = 0.0;
+        } else {
+            double x[D];
+#pragma unroll
+            for (int k = 0; k < D; ++k)
+                if (k < d) x[k] = p[(size_t)k * TILE];
+            if constexpr (MSA) {
+                double m1 = __builtin_inf(), m2 = __builtin_inf();
+                int32_t i1 = -1;
+                uint32_t neg = 0;
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    if (k < d) {
+                        const double av = __builtin_fabs(x[k]);
+                        neg ^= (x[k] >= 0) ? 0u : 1u;
+                        if (av < m1) { m1 = av; i1 = k; }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    if (k < d) {
+                        const double av = __builtin_fabs(x[k]);
+                        if (k != i1 && av < m2) m2 = av;
+                    }
+                }
+                const double a0 = __builtin_fabs(x[0]), a1 = __builtin_fabs(x[1]);
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    if (k < d) {
+                        const double af = (k == 0) ? a1 : a0;
+                        double mag = (k == i1) ? m2 : m1;
+                        if (__builtin_isnan(af)) mag = af;
+                        const uint32_t nk = (x[k] >= 0) ? 0u : 1u;
+                        const int sign = ((neg ^ nk) & 1u) ? -1 : 1;
+                        p[(size_t)k * TILE] = (double)sign * mag;
+                    }
+                }
+            } else {
+                check_bp_compute_rt<D, true>(x, d, p);
+            }
+        }
+    }
+    res_arrive(t, act, par, rs, ln0, b0, gridDim.x);
+}
+
 // Continuous mode for column degrees <= D (codes other than the
-// (8, 72)-regular one): var_m_block's lane handling -- finished lanes' outputs
+// (8, 72)-regular one; INPLACE: the resident pool, v2c == c2v, every load of
+// the column's edges ahead of its first store): var_m_block's lane handling -- finished lanes' outputs
 // first, refilled lanes' Init_Belief_Propagation (dec.cpp:608-629) /
 // Init_MSA_INF (dec.cpp:1300-1329), live lanes' update as k_var_bp_gr /
 // k_var_msa_gr -- for one column per wave with the degree read from col_ptr.
 // PC: coded priors (Refill::pcode / ptab, refills from Refill::in_code).
-template <bool MSA, int D, bool PC>
-__global__ __launch_bounds__(256) void k_var_gr_cont(const double* __restrict__ c2v, double* __restrict__ v2c,
+template <bool MSA, int D, bool PC, bool INPLACE = false>
+__global__ __launch_bounds__(256) void k_var_gr_cont(typename Msg<INPLACE>::in c2v, typename Msg<INPLACE>::out v2c,
                                                      double* __restrict__ prior, uint64_t* __restrict__ hard,
                                                      const uint64_t* __restrict__ active,
                                                      const int32_t* __restrict__ col_ptr,
@@ -1331,7 +1416,7 @@ __global__ __launch_bounds__(256) void k_var_gr_cont(const double* __restrict__ 
     }
     const int32_t a = col_ptr[j], d = col_ptr[j + 1] - a;
     const size_t tb = (size_t)t * E;
-    const double* __restrict__ c2v_t = c2v + (size_t)blockIdx.y * E * TILE;
+    typename Msg<INPLACE>::in c2v_t = c2v + (size_t)blockIdx.y * E * TILE;
     int32_t eid[D];
 #pragma unroll
     for (int s = 0; s < D; ++s)

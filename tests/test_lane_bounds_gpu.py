@@ -50,11 +50,13 @@ def test_bad_lane_index_is_reported_not_written(gpu, og, codewords, algo, sch):
 
 
 @pytest.mark.timeout(120)
-@pytest.mark.parametrize("algo", ["bp", "msa"])
-def test_bad_lane_index_generic_code(gpu, oracle_mod, tmp_path, algo):
+@pytest.mark.parametrize("algo,sch", [("bp", {}), ("msa", {}), ("bp", {"resident": False}),
+                                      ("msa", {"resident": False})])
+def test_bad_lane_index_generic_code(gpu, oracle_mod, tmp_path, algo, sch):
     """A code other than the (8, 72)-regular one in the continuous pool
-    (k_syndrome_split_gen's bookkeeping, k_var_gr_cont's guarded refill and
-    output accesses), fp64 and coded input."""
+    (the bookkeeping of k_check_gr_res (resident) or k_syndrome_split_gen
+    (grouped), k_var_gr_cont's guarded refill and output accesses), fp64 and
+    coded input."""
     L = gpu
     G2 = L.Graph.rs_ldpc(6, 32, 4)
     path = tmp_path / "rs.pchk"
@@ -69,10 +71,10 @@ def test_bad_lane_index_generic_code(gpu, oracle_mod, tmp_path, algo):
                 lambda sch: G2.decode_codes(codes, table, max_iter=8, algo=algo, post="llr", chunk=256,
                                             schedule=sch)):
         with pytest.raises(L.LdpcError) as e:
-            run({"debug_bad_lane": True})
+            run(dict(sch, debug_bad_lane=True))
         assert e.value.code == L.LDPC_ERR_DEVICE, str(e.value)
         _fault_message(str(e.value), B)
-        h, _, it, v = run({})
+        h, _, it, v = run(sch)
         rh, _, rit, rv = og2.decode_batch(llr, 8, algo=0 if algo == "bp" else 1, threads=8, want_post=False)
         assert np.array_equal(h, rh) and np.array_equal(it, rit) and np.array_equal(v, rv.astype(bool))
 

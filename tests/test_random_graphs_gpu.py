@@ -215,20 +215,30 @@ def test_generic_bucket_edges_bitexact(gpu, oracle_mod, tmp_path, case):
         _cmp_nan(G, og, llr, 20, algo="msa", schedule=sch)
 
 
-GEN_SCHEDULES = [{}, {"continuous": False}, {"group_tiles": 1}, {"syn_blocks": 1}, {"syn_blocks": 64, "group_tiles": 2}]
+GEN_SCHEDULES = [
+    {},                                                            # resident pool (k_check_gr_res, in place)
+    {"_chunk": 0},                                                 # the engine's own pool size (gen_pool_tiles)
+    {"resident": True, "pool_tiles": 1, "poll_every": 3, "_chunk": 0},
+    {"continuous": False},                                         # fixed passes
+    {"resident": False},                                           # grouped continuous
+    {"resident": False, "group_tiles": 1, "syn_blocks": 1},
+    {"resident": False, "syn_blocks": 64, "group_tiles": 2},
+]
 
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("sch", range(len(GEN_SCHEDULES)))
 def test_generic_continuous_bitexact(gpu, oracle_mod, tmp_path, sch):
     """Codes other than the (8, 72)-regular one in the continuous lane pool
-    (k_var_gr_cont, k_syndrome_split_gen): an RS-LDPC code (RS_LDPC.c) and an
+    (k_var_gr_cont; k_syndrome_split_gen or, resident, k_check_gr_res): an
+    RS-LDPC code (RS_LDPC.c) and an
     irregular random code, early-exiting BSC words in a batch several times
     the pool (lanes refilled as codewords finish), fp64 and int8-coded input,
     posteriors of every finished codeword -- equal to the oracle, and to the
     fixed-pass schedule."""
     rng = np.random.default_rng(900 + sch)
-    schedule = GEN_SCHEDULES[sch]
+    schedule = dict(GEN_SCHEDULES[sch])
+    chunk = schedule.pop("_chunk", 256)
     rows, cols = _random_graph(rng, 90, 700, 4, 40)
     path = tmp_path / "irr.pchk"
     _write_pchk(path, 90, 700, rows, cols)
@@ -250,7 +260,7 @@ def test_generic_continuous_bitexact(gpu, oracle_mod, tmp_path, sch):
             a = 0 if algo == "bp" else 1
             post = "ratio" if a == 0 else "llr"
             rh, rp, rit, rv = og.decode_batch(llr, 30, algo=a, post_mode=1 if a == 0 else 0, threads=8)
-            eng_kw = dict(max_iter=30, algo=algo, post=post, schedule=schedule, chunk=256)
+            eng_kw = dict(max_iter=30, algo=algo, post=post, schedule=schedule, chunk=chunk)
             h, pp, it, v = G.decode(llr, **eng_kw)
             assert np.array_equal(h, rh) and np.array_equal(it, rit) and np.array_equal(v, rv.astype(bool)), algo
             assert np.array_equal(pp.view(np.uint64), rp.view(np.uint64)), algo

@@ -43,10 +43,11 @@ def main():
     ap.add_argument("--p", type=float, default=0.05)
     ap.add_argument("--chunk", type=int, default=0, help="lane pool / pass size (default: the batch)")
     ap.add_argument("--fixed", action="store_true", help="fixed passes instead of the continuous lane pool")
+    ap.add_argument("--pool", action="store_true", help="the engine's default pool (resident where it applies)")
     ap.add_argument("--only", default="", help="substring of the code names to run")
     a = ap.parse_args()
     import ldpc_amd as L
-    print(f"{'code':32s} {'N':>6} {'M':>5} {'E':>7} {'dv':>3} {'dc':>3} {'path':>10} {'cw/s':>10} "
+    print(f"{'code':32s} {'N':>6} {'M':>5} {'E':>7} {'dv':>3} {'dc':>3} {'path':>14} {'cw/s':>10} "
           f"{'it/cw':>6} {'GB/s':>7} {'frac':>6} {'chk us':>7} {'var us':>7} {'syn us':>7}", flush=True)
     for name, G in codes(L, None):
         if a.only and a.only not in name:
@@ -55,7 +56,7 @@ def main():
         # a few GB of state at most (with --chunk the state is the pool's; the batch as given)
         B = a.batch if a.chunk > 0 else max(64, min(a.batch, int(4e9 // (E * 16 + N * 10))))
         kw = {"continuous": False} if a.fixed else {}
-        eng = L.Engine(G, 0, a.algo, chunk=min(B, a.chunk) if a.chunk > 0 else B, **kw)
+        eng = L.Engine(G, 0, a.algo, chunk=0 if a.pool else min(B, a.chunk) if a.chunk > 0 else B, **kw)
         cw = np.zeros((1, N), np.uint8)
         d_cw = L.DeviceBuffer(0, N)
         d_cw.upload(cw)
@@ -85,7 +86,8 @@ def main():
             return st[k]["ms"] / st[k]["sampled"] * 1e3 if st[k]["sampled"] else 0.0
         gbs = (32.0 * E + 10.0 * N) * cwi / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         path = "72/8" if (G.dc == 72 and G.dv == 8 and G.regular_dc and G.regular_dv) else "generic"
-        print(f"{name:32s} {N:>6} {G.M:>5} {E:>7} {G.dv:>3} {G.dc:>3} {path:>10} {B / el:>10.1f} "
+        path += "/res" if eng.resident else "/grp" if eng.continuous else "/fix"
+        print(f"{name:32s} {N:>6} {G.M:>5} {E:>7} {G.dv:>3} {G.dc:>3} {path:>14} {B / el:>10.1f} "
               f"{cwi / B:>6.1f} {gbs:>7.1f} {gbs / 8000:>6.3f} {per('check'):>7.1f} {per('variable'):>7.1f} "
               f"{per('syndrome'):>7.1f}", flush=True)
         for b in (d_cw, d_in, d_h, d_i, d_v):
