@@ -87,8 +87,9 @@ enum {
     LDPC_SCHED_MSA_COMPRESSED = 1 << 4, /* min-sum check->variable messages as per-row records (min1, min2,
                                            NaN planes) + one 16-bit meta word per row and codeword
                                            ((8,72)-regular graphs with E < 2^18; default on) */
-    LDPC_SCHED_RESIDENT = 1 << 5,       /* continuous BP / fp64 min-sum on (8,72)-regular graphs with N % 32 == 0:
-                                           a pool of pool_tiles tiles iterated
+    LDPC_SCHED_RESIDENT = 1 << 5,       /* continuous BP / fp64 min-sum on (8,72)-regular graphs with N % 32 == 0
+                                           or graphs with rows <= 96 and columns <= 16: a pool of pool_tiles tiles
+                                           iterated
                                            in place, its state sized to the 256 MB Infinity Cache, the
                                            syndrome fused into the check kernel (default on when the lane
                                            pool is chosen by the engine or is at most 4 tiles) */
@@ -116,7 +117,8 @@ typedef struct ldpc_schedule {
     int32_t var_cpw;     /* columns per variable-phase wavefront: 1, 2, 4 or 8 (3: compressed min-sum only;
                             0 = default: 2 for coded input in the resident pool or the compressed
                             min-sum, else 4) */
-    int32_t pool_tiles;  /* resident pool tiles when the engine chooses the pool (0 = default 3) */
+    int32_t pool_tiles;  /* resident pool tiles when the engine chooses the pool (0 = default: 3 for the
+                            (8,72)-regular kernels, else as many as fit ~226 MB of messages + priors) */
     int32_t poll_every;  /* resident pool: steps between occupancy polls (0 = default 8) */
     int32_t syn_blocks;  /* continuous grouped schedule: syndrome blocks per tile (0 = default 32) */
     int32_t reserved;    /* 0 */
