@@ -222,6 +222,12 @@ int Engine::init(const HostGraph* graph, int dev, int algorithm, int64_t chunk, 
     // grouped schedule (A/B, 272-codeword DNA batch at cap 320: 193k -> 250k cw/s)
     const bool res_chosen = (sched.flags_set & kResChosen) != 0;
     if (res && !res_chosen && chunk > kResAutoMaxTiles * 64) res = false;
+    // an (8, 72)-regular code larger than the DNA code: its default 3-tile pool
+    // would overflow the Infinity Cache (RS(9,72,8), N = 36 864: 509 MB, 12 %
+    // slower than the grouped schedule, profiles/r6/generic_codes.txt)
+    if (res && !res_chosen && reg_72_8 && sched.pool_tiles <= 0 &&
+        64.0 * 8.0 * kDefaultPoolTiles * ((double)g->E + (double)g->N) > 1.15 * kGenPoolBytes)
+        res = false;
     nt_d = sched_flag(sched, LDPC_SCHED_NONTEMPORAL) && !res;  // the pool is meant to stay cached
     debug_no_drain = sched_flag(sched, LDPC_SCHED_DEBUG_NO_DRAIN);
     debug_bad_lane = sched_flag(sched, LDPC_SCHED_DEBUG_BAD_LANE);
