@@ -160,7 +160,7 @@ static uint16_t* msa_meta(double* scratch, int64_t tiles, int32_t M)
 // (the memory-staged *_gen kernels then run; no continuous mode without a
 // variable bucket).
 static constexpr int kGenCheckBuckets[] = {8, 16, 32, 48, 64, 96, 0};
-static constexpr int kGenVarBuckets[] = {4, 8, 12, 16, 0};
+static constexpr int kGenVarBuckets[] = {4, 8, 12, 16, 24, 32, 0};
 static int gen_bucket(int32_t dmax, const int* buckets)
 {
     for (const int* b = buckets; *b; ++b)
@@ -667,7 +667,7 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
     // generic column degrees: registers up to the bucket of dv_max, else memory
     const int vb = gen_bucket(g->dv_max, kGenVarBuckets);
     if (cnt) {
-        if (!vb) { set_error("continuous mode needs column degrees <= 16"); return LDPC_ERR_ARG; }
+        if (!vb) { set_error("continuous mode needs column degrees <= 32"); return LDPC_ERR_ARG; }
         const bool pc = rf.in_code != nullptr;
         const bool inplace = scratch == v2c;  // the resident pool
 #define VAR_GRC3(MSA, D, PC)                                                                                         \
@@ -685,7 +685,9 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
             if (vb == 4) VAR_GRC(4);
             else if (vb == 8) VAR_GRC(8);
             else if (vb == 12) VAR_GRC(12);
-            else VAR_GRC(16);
+            else if (vb == 16) VAR_GRC(16);
+            else if (vb == 24) VAR_GRC(24);
+            else VAR_GRC(32);
         });
 #undef VAR_GRC
 #undef VAR_GRC2
@@ -703,7 +705,9 @@ int Engine::launch_var(hipStream_t s, double* scratch, int64_t t0, unsigned gt, 
             if (vb == 4) VAR_GR(4);
             else if (vb == 8) VAR_GR(8);
             else if (vb == 12) VAR_GR(12);
-            else VAR_GR(16);
+            else if (vb == 16) VAR_GR(16);
+            else if (vb == 24) VAR_GR(24);
+            else VAR_GR(32);
         });
 #undef VAR_GR
         return LDPC_OK;

@@ -82,13 +82,13 @@ enum {
                                            variable->check stream (default on) */
     LDPC_SCHED_CONTINUOUS = 1 << 3,     /* continuous batching: a finished codeword's lane is refilled with
                                            the next one (fp64 decoders on graphs whose column degrees are all
-                                           <= 16, or (8,72)-regular; default on; needs hard / iters / valid
+                                           <= 32, or (8,72)-regular; default on; needs hard / iters / valid
                                            outputs) */
     LDPC_SCHED_MSA_COMPRESSED = 1 << 4, /* min-sum check->variable messages as per-row records (min1, min2,
                                            NaN planes) + one 16-bit meta word per row and codeword
                                            ((8,72)-regular graphs with E < 2^18; default on) */
     LDPC_SCHED_RESIDENT = 1 << 5,       /* continuous BP / fp64 min-sum on (8,72)-regular graphs with N % 32 == 0
-                                           or graphs with rows <= 96 and columns <= 16: a pool of pool_tiles tiles
+                                           or graphs with rows <= 96 and columns <= 32: a pool of pool_tiles tiles
                                            iterated
                                            in place, its state sized to the 256 MB Infinity Cache, the
                                            syndrome fused into the check kernel (default on when the lane

@@ -191,7 +191,7 @@ def _bucket_graph(rng, M, N, dc_max, dv_max):
 
 
 BUCKETS = [(8, 4), (9, 5), (16, 8), (17, 9), (32, 12), (33, 13), (48, 16), (49, 17), (64, 3), (65, 2), (96, 16),
-           (97, 17)]
+           (97, 17), (40, 24), (41, 25), (60, 32), (61, 33)]
 
 
 @pytest.mark.timeout(600)
