@@ -1,13 +1,19 @@
 """Throughput of the decoder on codes other than the DNA code (not part of
 the product): RS-LDPC codes from the native constructor (RS_LDPC.c
 parameters), random regular and irregular codes.  BP (and min-sum) on BSC
-words of the all-zero codeword, p chosen so that most words run all
-iterations, device-resident engine, 1 warm-up + 2 timed decodes.  Prints
-codewords/s, the kernel path (specialised or generic) and the iteration's
-algorithmic bytes (32 E + 10 N per codeword-iteration) over the
-kernel time, against 8 TB/s.
+words of the all-zero codeword (--p; the default 0.05 makes most words run
+all iterations), device-resident engine, 1 warm-up + 2 timed decodes.
+Prints codewords/s, the kernel path (specialised 72/8 or generic; resident,
+grouped continuous or fixed passes), the iteration's algorithmic bytes
+(32 E + 10 N per codeword-iteration) over the kernel time
+against 8 TB/s, and the sampled per-launch kernel times.
 
-    python tools/code_bench.py [--batch 8192] [--iters 30]
+    python tools/code_bench.py [--batch 8192] [--iters 30] [--algo bp|msa] [--p 0.05]
+                               [--chunk LANES | --pool] [--fixed] [--only SUBSTRING]
+
+--chunk sets the lane pool / pass size (default: the whole batch), --pool
+takes the engine's own default pool (resident where it applies), --fixed
+runs fixed passes.
 """
 import argparse
 import os
